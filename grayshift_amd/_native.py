@@ -1,0 +1,159 @@
+"""ctypes mirror of include/grayshift_scene.h, grayshift_gpu.h and grayshift_host.h.
+
+Loads the in-tree ``libgrayshift.so``.  There is no fallback: if the library is
+missing or fails to load, importing this module raises — the product path is the
+HIP extension or nothing.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgrayshift.so")
+
+# ------------------------------------------------------------------ enums
+GS_OBJ_SPHERE, GS_OBJ_MOVING_SPHERE, GS_OBJ_QUAD, GS_OBJ_TRIANGLE = 1, 2, 3, 4
+GS_OBJ_LIST, GS_OBJ_BVH, GS_OBJ_TRANSLATE, GS_OBJ_ROTATE_Y, GS_OBJ_CUBE = 5, 6, 7, 8, 9
+GS_MAT_LAMBERTIAN, GS_MAT_METAL, GS_MAT_DIELECTRIC, GS_MAT_DIFFUSE_LIGHT, GS_MAT_ISOTROPIC = 1, 2, 3, 4, 5
+GS_TEX_SOLID, GS_TEX_CHECKERED, GS_TEX_IMAGE = 1, 2, 3
+GS_BG_SOLID, GS_BG_HDRI = 1, 2
+GS_OK, GS_ERR_ARG, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPORTED, GS_ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5
+
+D3 = C.c_double * 3
+
+
+class gs_object(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("material", C.c_int32), ("first", C.c_int32), ("count", C.c_int32),
+                ("p", C.c_double * 9)]
+
+
+class gs_material_spec(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("texture", C.c_int32), ("p", C.c_double * 4)]
+
+
+class gs_texture_spec(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("a", C.c_int32), ("b", C.c_int32), ("pad", C.c_int32),
+                ("p", C.c_double * 3)]
+
+
+class gs_image_spec(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("rgb8", C.c_void_p)]
+
+
+class gs_background_spec(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("width", C.c_int32), ("height", C.c_int32), ("pad", C.c_int32),
+                ("color", D3), ("rotation", D3), ("rgb", C.c_void_p)]
+
+
+class gs_scene_spec(C.Structure):
+    _fields_ = [("objects", C.POINTER(gs_object)), ("n_objects", C.c_int32),
+                ("children", C.POINTER(C.c_int32)), ("n_children", C.c_int32),
+                ("world", C.POINTER(C.c_int32)), ("n_world", C.c_int32),
+                ("materials", C.POINTER(gs_material_spec)), ("n_materials", C.c_int32),
+                ("textures", C.POINTER(gs_texture_spec)), ("n_textures", C.c_int32),
+                ("images", C.POINTER(gs_image_spec)), ("n_images", C.c_int32),
+                ("background", gs_background_spec)]
+
+
+class gs_camera_spec(C.Structure):
+    _fields_ = [("aspect_ratio", C.c_double), ("image_width", C.c_int32), ("max_depth", C.c_uint32),
+                ("v_fov", C.c_double), ("look_from", D3), ("look_at", D3), ("vup", D3),
+                ("defocus_angle", C.c_double), ("focus_distance", C.c_double)]
+
+
+class gs_sample_settings(C.Structure):
+    _fields_ = [("confidence", C.c_double), ("tolerance", C.c_double), ("batch_size", C.c_uint32),
+                ("max_samples", C.c_uint32)]
+
+
+COUNTER_NAMES = ["rays", "node_visits", "sphere_tests", "msphere_tests", "quad_tests", "tri_tests",
+                 "instance_tests", "list_tests", "hits", "image_texels", "hdri_texels", "paths", "pixels"]
+
+
+class gs_counters(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in COUNTER_NAMES] + [("reserved", C.c_uint64 * 3)]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n in COUNTER_NAMES}
+
+
+class gs_camera(C.Structure):
+    _fields_ = [("image_width", C.c_int32), ("image_height", C.c_int32), ("max_depth", C.c_uint32),
+                ("pad", C.c_uint32), ("center", D3), ("starting_pixel_pos", D3), ("pixel_delta_u", D3),
+                ("pixel_delta_v", D3), ("defocus_angle", C.c_double), ("defocus_disk_u", D3),
+                ("defocus_disk_v", D3)]
+
+
+class gs_partition(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("world_size", C.c_int32), ("tile_w", C.c_int32), ("tile_h", C.c_int32)]
+
+
+class gs_flat_scene(C.Structure):  # only counts are read from Python
+    _fields_ = [("root", C.c_uint32), ("max_bvh_depth", C.c_uint32),
+                ("nodes", C.c_void_p), ("n_nodes", C.c_uint32),
+                ("spheres", C.c_void_p), ("n_spheres", C.c_uint32),
+                ("mspheres", C.c_void_p), ("n_mspheres", C.c_uint32),
+                ("quads", C.c_void_p), ("n_quads", C.c_uint32),
+                ("triangles", C.c_void_p), ("n_triangles", C.c_uint32),
+                ("lists", C.c_void_p), ("n_lists", C.c_uint32),
+                ("list_refs", C.c_void_p), ("n_list_refs", C.c_uint32),
+                ("instances", C.c_void_p), ("n_instances", C.c_uint32),
+                ("materials", C.c_void_p), ("n_materials", C.c_uint32),
+                ("textures", C.c_void_p), ("n_textures", C.c_uint32),
+                ("images", C.c_void_p), ("n_images", C.c_uint32),
+                ("texels8", C.c_void_p), ("n_texels8", C.c_uint64)]
+
+
+# Every symbol include/*.h declares, with its ctypes signature.
+_P = C.c_void_p
+SIGNATURES = {
+    # grayshift_gpu.h
+    "gs_last_error": (C.c_char_p, []),
+    "gs_version": (C.c_int32, []),
+    "gs_set_tuning": (C.c_int32, [C.c_int32, C.c_int32]),
+    "gs_device_scene_create": (C.c_int32, [_P, C.POINTER(_P)]),
+    "gs_device_scene_destroy": (C.c_int32, [_P]),
+    "gs_partition_capacity": (C.c_int64, [C.POINTER(gs_camera), C.POINTER(gs_partition)]),
+    "gs_render_tiles_async": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64,
+                                          C.POINTER(gs_partition), _P, _P, _P]),
+    "gs_unpack_tiles_async": (C.c_int32, [C.POINTER(gs_camera), C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P, _P,
+                                          _P]),
+    "gs_render": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64, _P,
+                              C.POINTER(gs_counters)]),
+    # grayshift_host.h
+    "gs_host_scene_from_spec": (C.c_int32, [C.POINTER(gs_scene_spec), C.POINTER(_P)]),
+    "gs_host_scene_destroy": (C.c_int32, [_P]),
+    "gs_host_scene_flat": (_P, [_P]),
+    "gs_host_camera": (C.c_int32, [C.POINTER(gs_camera_spec), C.POINTER(gs_camera)]),
+    "gs_host_render_spec": (C.c_int32, [C.POINTER(gs_scene_spec), C.POINTER(gs_camera_spec),
+                                        C.POINTER(gs_sample_settings), C.c_uint64, _P, C.POINTER(gs_counters)]),
+    "gs_host_write_ppm": (C.c_int32, [C.c_char_p, C.c_int32, C.c_int32, _P]),
+    "gs_host_color_byte": (C.c_int32, [C.c_double]),
+    "gs_host_bvh_topology": (C.c_int64, [C.POINTER(gs_scene_spec), C.POINTER(C.c_int32), C.c_int64]),
+    "gs_host_struct_size": (C.c_int64, [C.c_char_p]),
+}
+
+
+class GrayshiftError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("grayshift error %d: %s" % (code, msg))
+        self.code = code
+
+
+def load(path=LIB_PATH):
+    if not os.path.exists(path):
+        raise ImportError("libgrayshift.so not built (%s): run `python -m grayshift_amd.build`" % path)
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = load()
+
+
+def check(status):
+    if status != GS_OK:
+        raise GrayshiftError(status, lib.gs_last_error().decode("utf-8", "replace"))
+    return status

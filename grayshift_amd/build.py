@@ -1,0 +1,99 @@
+"""Build the in-tree native libraries.
+
+* ``grayshift_amd/libgrayshift.so`` — the product: HIP megakernel for gfx950 plus
+  the C++ host mirror, one shared library (hipcc; no torch, no JIT cache).
+* ``oracle/liboracle.so`` — the CPU checker (test infrastructure; g++ via
+  oracle/Makefile).
+
+Both are compiled with ``-ffp-contract=off``: the reference's Rust f64 code
+never fuses multiply-add, and neither may we.
+
+Usage: python -m grayshift_amd.build [--force] [--no-oracle]
+"""
+import argparse
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "libgrayshift.so")
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+
+SOURCES = [
+    os.path.join(HERE, "csrc", "device", "render.hip"),
+    os.path.join(HERE, "csrc", "host", "world.cpp"),
+    os.path.join(HERE, "csrc", "host", "camera.cpp"),
+    os.path.join(HERE, "csrc", "host", "host_capi.cpp"),
+]
+DEPS = SOURCES + [
+    os.path.join(HERE, "csrc", "device", "devmath.hpp"),
+    os.path.join(HERE, "csrc", "host", "world.hpp"),
+    os.path.join(ROOT, "include", "grayshift_gpu.h"),
+    os.path.join(ROOT, "include", "grayshift_host.h"),
+    os.path.join(ROOT, "include", "grayshift_scene.h"),
+]
+
+ARCH = os.environ.get("GS_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall",
+          "-Wno-unused-parameter", "-Wno-unused-variable"]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build_product(force=False, verbose=False, extra=()):
+    if not force and not _stale(LIB, DEPS):
+        return LIB
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(HERE, "csrc", "_obj", os.path.basename(src) + ".o")
+        os.makedirs(os.path.dirname(obj), exist_ok=True)
+        cmd = [HIPCC] + COMMON + list(extra)
+        if src.endswith(".hip"):
+            cmd += ["-x", "hip", "--offload-arch=" + ARCH]
+        cmd += ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    tmp = LIB + ".tmp"
+    cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", tmp] + objs + ["-lpthread"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(force=False, verbose=False):
+    if force and os.path.exists(ORACLE_LIB):
+        os.remove(ORACLE_LIB)
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True,
+                   stdout=None if verbose else subprocess.DEVNULL)
+    return ORACLE_LIB
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--no-oracle", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--resource-usage", action="store_true",
+                    help="print per-kernel VGPR/SGPR/LDS/occupancy (hipcc remarks)")
+    a = ap.parse_args(argv)
+    extra = ["-Rpass-analysis=kernel-resource-usage"] if a.resource_usage else []
+    build_product(force=a.force or a.resource_usage, verbose=a.verbose, extra=extra)
+    if not a.no_oracle:
+        build_oracle(force=a.force, verbose=a.verbose)
+    print("built", LIB, "" if a.no_oracle else ORACLE_LIB)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,1153 @@
+// render.hip — persistent-wavefront path-tracing megakernel for gfx950 (MI355X),
+// and the device half of the C-ABI in include/grayshift_gpu.h.
+//
+// What it replaces: the reference's per-pixel loop camera.rs:105-114 →
+// Camera::sample (camera.rs:125-171) → recursive Camera::ray_color (:174-202) →
+// BVHNode::hit (BVH.rs:69-90) / AABB::hit (AABB.rs:58-113) / primitive hits →
+// Material::scatter (material.rs) → Texture::value_at / HDRI::sample.
+//
+// Structure:
+//  * one lane owns one pixel and runs all of its samples in the reference's order,
+//    so the per-pixel sums accumulate exactly as camera.rs:138-147 does;
+//  * a wave pulls pixels from an atomic work queue when lanes finish (ballot +
+//    popcount + one atomicAdd per wave), so sky pixels never wait for busy ones;
+//  * each lane runs a small state machine NEED → TRACE → SHADE → (TRACE | NEED):
+//    the wave keeps stepping BVH traversal until `shade_batch` lanes have finished
+//    their ray, then shades those lanes together (active-ray packing) while the
+//    others keep their traversal state (current ref + LDS stack) for the next round;
+//  * traversal is the reference's left-first DFS with a global closest-t, restated
+//    as an explicit stack in LDS ([depth][lane], conflict-free), identical in node
+//    visits and primitive tests;
+//  * the hit record is recomputed once per ray from (primitive, t) after traversal,
+//    which yields the same values the reference computes at every accepted hit.
+// All arithmetic is f64 with -ffp-contract=off, as the reference's Rust.
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../../include/grayshift_gpu.h"
+#include "devmath.hpp"
+
+using namespace gsd;
+
+#define GS_BLOCK 256
+#define GS_STACK 32
+#define GS_MAX_CHAIN 4
+
+// ---------------------------------------------------------------- device layout
+// Internal layouts (may differ from the ABI records; converted at upload).
+struct alignas(16) DNode {  // 64 B: box (f64, as AABB.rs) + children
+    double mnx, mny, mnz, mxx, mxy, mxz;
+    uint32_t left, right, pad0, pad1;
+};
+struct alignas(16) DSphere {  // 32 B: what Sphere::hit reads; material kept apart
+    double cx, cy, cz, r;
+};
+struct alignas(16) DMaterial {
+    uint32_t kind, texture, needs_uv, pad;
+    double albedo[3];
+    double param;
+};
+
+enum { C_RAYS = 0, C_NODES, C_SPH, C_MSPH, C_QUAD, C_TRI, C_INST, C_LIST, C_HITS, C_IMG, C_HDRI, C_PATHS, C_PIX, C_N };
+
+struct DevScene {
+    const DNode* nodes;
+    const DSphere* spheres;
+    const uint32_t* sphere_mat;
+    const gs_msphere* mspheres;
+    const gs_quad* quads;
+    const gs_triangle* tris;
+    const gs_list* lists;
+    const uint32_t* list_refs;
+    const gs_instance* inst;
+    const DMaterial* mats;
+    const gs_texture* texs;
+    const gs_image* images;
+    const uint8_t* texels;
+    const float* hdri;
+    gs_background bg;
+    uint32_t root;
+};
+
+struct KArgs {
+    DevScene sc;
+    gs_camera cam;
+    gs_sample_settings ss;
+    uint64_t seed;
+    int32_t rank, world_size, tile_w, tile_h, tiles_x, shade_batch;
+    uint32_t capacity;
+    float* out;
+    unsigned long long* counters;
+    uint32_t* queue;
+};
+
+enum { S_NEED = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };
+
+struct Ray {
+    d3 o, d;
+    double time;
+};
+
+// AABB::hit (AABB.rs:58-113) with the reference's 1.0/d hoisted per ray (same value).
+// The early-outs of the reference do not change the boolean: once max <= min the
+// later slabs only raise min / lower max, and NaN slabs never assign.
+__device__ __forceinline__ bool box_hit(const DNode& n, const d3& o, const d3& inv, double tmin, double tmax) {
+    double lo = tmin, hi = tmax;
+    {
+        double t0 = (n.mnx - o.x) * inv.x, t1 = (n.mxx - o.x) * inv.x;
+        bool s = t0 < t1;
+        double a = s ? t0 : t1, b = s ? t1 : t0;
+        if (a > lo) lo = a;
+        if (b < hi) hi = b;
+    }
+    {
+        double t0 = (n.mny - o.y) * inv.y, t1 = (n.mxy - o.y) * inv.y;
+        bool s = t0 < t1;
+        double a = s ? t0 : t1, b = s ? t1 : t0;
+        if (a > lo) lo = a;
+        if (b < hi) hi = b;
+    }
+    {
+        double t0 = (n.mnz - o.z) * inv.z, t1 = (n.mxz - o.z) * inv.z;
+        bool s = t0 < t1;
+        double a = s ? t0 : t1, b = s ? t1 : t0;
+        if (a > lo) lo = a;
+        if (b < hi) hi = b;
+    }
+    return !(hi <= lo);
+}
+
+// Sphere::hit acceptance (sphere.rs:64-88): returns t or a NaN-free miss flag.
+__device__ __forceinline__ bool sphere_accept(d3 c, double r, const Ray& ray, double a, double tmin, double tmax,
+                                         double& t_out) {
+    d3 oc = sub(c, ray.o);
+    double h = dot(ray.d, oc);
+    double cc = len2(oc) - r * r;
+    double disc = h * h - a * cc;
+    if (disc < 0.0) return false;
+    double sq = sqrt(disc);
+    double t = (h - sq) / a;
+    if (!(tmin < t && t < tmax)) {
+        t = (h + sq) / a;
+        if (!(tmin < t && t < tmax)) return false;
+    }
+    t_out = t;
+    return true;
+}
+
+// Quad::hit acceptance (quad.rs:84-95, plane.rs:20-32).
+__device__ __forceinline__ bool quad_accept(const gs_quad& q, const Ray& ray, double tmin, double tmax, double& t_out) {
+    d3 nrm = ld3(q.normal);
+    double den = dot(nrm, ray.d);
+    if (fabs(den) < 1e-8) return false;
+    double t = (q.d - dot(nrm, ray.o)) / den;
+    if (!(tmin <= t && t <= tmax)) return false;
+    d3 inter = add(ray.o, muls(ray.d, t));
+    d3 planar = sub(inter, ld3(q.q));
+    double alpha = dot(ld3(q.w), cross(planar, ld3(q.v)));
+    double beta = dot(ld3(q.w), cross(ld3(q.u), planar));
+    if (!(0.0 <= alpha && alpha <= 1.0) || !(0.0 <= beta && beta <= 1.0)) return false;
+    t_out = t;
+    return true;
+}
+
+// Triangle::hit (triangle.rs:34-68): one-sided, ray_t ignored (reference quirk).
+__device__ __forceinline__ bool tri_hit(const gs_triangle& tr, const Ray& ray, double& t_out, double& u_out,
+                                        double& v_out) {
+    d3 a = ld3(tr.a);
+    d3 e1 = sub(ld3(tr.c), a), e2 = sub(ld3(tr.b), a);
+    d3 p_vec = cross(ray.d, e2);
+    double det = dot(e1, p_vec);
+    if (det < 1e-8) return false;
+    d3 t_vec = sub(ray.o, a);
+    double u = dot(t_vec, p_vec);
+    if (u < 0.0 || u > det) return false;
+    d3 q_vec = cross(t_vec, e1);
+    double v = dot(ray.d, q_vec);
+    if (v < 0.0 || u + v > det) return false;
+    double t = dot(e2, q_vec);
+    double inv_det = 1.0 / det;
+    t_out = t * inv_det;
+    u_out = u * inv_det;
+    v_out = v * inv_det;
+    return true;
+}
+
+// Translate/RotateY forward ray transforms (hittable.rs:107-113, :179-193).
+__device__ __forceinline__ void inst_forward(const gs_instance& in, Ray& r) {
+    if (in.kind == GS_INST_TRANSLATE) {
+        r.o = sub(r.o, ld3(in.p));
+    } else {
+        double s = in.p[0], c = in.p[1];
+        r.o = mk((c * r.o.x) - (s * r.o.z), r.o.y, (s * r.o.x) + (c * r.o.z));
+        r.d = mk((c * r.d.x) - (s * r.d.z), r.d.y, (s * r.d.x) + (c * r.d.z));
+    }
+}
+// Hit-record back transforms (hittable.rs:115-117, :195-207).
+__device__ __forceinline__ void inst_backward(const gs_instance& in, d3& p, d3& n) {
+    if (in.kind == GS_INST_TRANSLATE) {
+        p = add(p, ld3(in.p));
+    } else {
+        double s = in.p[0], c = in.p[1];
+        p = mk((c * p.x) + (s * p.z), p.y, (-s * p.x) + (c * p.z));
+        n = mk((c * n.x) + (s * n.z), n.y, (-s * n.x) + (c * n.z));
+    }
+}
+
+// Test one primitive ref against `ray` (already in the primitive's space).
+// Accepts -> closest/hit_ref updated ("last accepted wins", as BVH.rs:73-80 and
+// hittable.rs:75-83 compose).
+__device__ __forceinline__ void prim_test(const DevScene& sc, uint32_t ref, const Ray& ray, double tmin,
+                                          double& closest, uint32_t& hit_ref, uint32_t& hit_inst, uint32_t inst_ref,
+                                          unsigned long long* cnt, uint32_t& c_sph) {
+    const uint32_t kind = ref >> GS_REF_SHIFT, idx = ref & GS_REF_MASK;
+    double t;
+    bool ok = false;
+    if (kind == GS_REF_SPHERE) {
+        c_sph++;
+        DSphere s = sc.spheres[idx];
+        ok = sphere_accept(mk(s.cx, s.cy, s.cz), s.r, ray, len2(ray.d), tmin, closest, t);
+    } else if (kind == GS_REF_MSPHERE) {
+        atomicAdd(&cnt[C_MSPH], 1ull);
+        const gs_msphere& s = sc.mspheres[idx];
+        d3 c = add(ld3(s.center_start), muls(ld3(s.center_path), ray.time));
+        ok = sphere_accept(c, s.radius, ray, len2(ray.d), tmin, closest, t);
+    } else if (kind == GS_REF_QUAD) {
+        atomicAdd(&cnt[C_QUAD], 1ull);
+        ok = quad_accept(sc.quads[idx], ray, tmin, closest, t);
+    } else if (kind == GS_REF_TRIANGLE) {
+        atomicAdd(&cnt[C_TRI], 1ull);
+        double u, v;
+        ok = tri_hit(sc.tris[idx], ray, t, u, v);
+    }
+    if (ok) {
+        closest = t;
+        hit_ref = ref;
+        hit_inst = inst_ref;
+    }
+}
+
+// A non-node child: primitive, list, or instance chain (→ list or primitive).
+__device__ __noinline__ void leaf_test(const DevScene& sc, uint32_t ref, const Ray& ray, double tmin, double& closest,
+                                       uint32_t& hit_ref, uint32_t& hit_inst, unsigned long long* cnt,
+                                       uint32_t& c_sph) {
+    uint32_t kind = ref >> GS_REF_SHIFT;
+    uint32_t inst_ref = GS_REF_NONE;
+    Ray r = ray;
+    uint32_t cur = ref;
+    if (kind == GS_REF_INSTANCE) {
+        inst_ref = ref;
+#pragma unroll 1
+        for (int k = 0; k < GS_MAX_CHAIN && (cur >> GS_REF_SHIFT) == GS_REF_INSTANCE; k++) {
+            const gs_instance& in = sc.inst[cur & GS_REF_MASK];
+            atomicAdd(&cnt[C_INST], 1ull);
+            inst_forward(in, r);
+            cur = in.child;
+        }
+        kind = cur >> GS_REF_SHIFT;
+    }
+    if (kind == GS_REF_LIST) {
+        atomicAdd(&cnt[C_LIST], 1ull);
+        const gs_list l = sc.lists[cur & GS_REF_MASK];
+#pragma unroll 1
+        for (uint32_t k = 0; k < l.count; k++)
+            prim_test(sc, sc.list_refs[l.first + k], r, tmin, closest, hit_ref, hit_inst, inst_ref, cnt, c_sph);
+    } else {
+        prim_test(sc, cur, r, tmin, closest, hit_ref, hit_inst, inst_ref, cnt, c_sph);
+    }
+}
+
+struct HitRec {
+    d3 p, n;
+    bool front;
+    double u, v;
+    uint32_t mat;
+};
+
+__device__ __forceinline__ void sphere_uv(d3 p, double& u, double& v) {  // sphere.rs:55-60
+    const double PI = 3.14159265358979323846;
+    double theta = acos(-p.y);
+    double phi = atan2(-p.z, p.x) + PI;
+    u = phi / (2.0 * PI);
+    v = theta / PI;
+}
+
+// Recompute the HitRecord of the accepted primitive at t (the values the reference
+// built when it accepted it), then apply the instance back-transforms innermost-first.
+__device__ __noinline__ void reconstruct(const DevScene& sc, const Ray& ray, double t, uint32_t hit_ref,
+                                         uint32_t hit_inst, HitRec& h) {
+    Ray r = ray;
+    uint32_t ch0 = 0, ch1 = 0, ch2 = 0, ch3 = 0;
+    int nch = 0;
+    if (hit_inst != GS_REF_NONE) {
+        uint32_t cur = hit_inst;
+#pragma unroll
+        for (int k = 0; k < GS_MAX_CHAIN; k++) {
+            if ((cur >> GS_REF_SHIFT) != GS_REF_INSTANCE) break;
+            uint32_t i = cur & GS_REF_MASK;
+            if (k == 0) ch0 = i; else if (k == 1) ch1 = i; else if (k == 2) ch2 = i; else ch3 = i;
+            nch = k + 1;
+            const gs_instance& in = sc.inst[i];
+            inst_forward(in, r);
+            cur = in.child;
+        }
+    }
+    const uint32_t kind = hit_ref >> GS_REF_SHIFT, idx = hit_ref & GS_REF_MASK;
+    d3 p, outward;
+    double u = 0.0, v = 0.0;
+    if (kind == GS_REF_SPHERE || kind == GS_REF_MSPHERE) {
+        d3 c;
+        double rad;
+        if (kind == GS_REF_SPHERE) {
+            DSphere s = sc.spheres[idx];
+            c = mk(s.cx, s.cy, s.cz);
+            rad = s.r;
+            h.mat = sc.sphere_mat[idx];
+        } else {
+            const gs_msphere& s = sc.mspheres[idx];
+            c = add(ld3(s.center_start), muls(ld3(s.center_path), r.time));
+            rad = s.radius;
+            h.mat = s.material;
+        }
+        p = add(r.o, muls(r.d, t));
+        outward = divs(sub(p, c), rad);
+        if (sc.mats[h.mat].needs_uv) sphere_uv(outward, u, v);
+    } else if (kind == GS_REF_QUAD) {
+        const gs_quad& q = sc.quads[idx];
+        p = add(r.o, muls(r.d, t));
+        d3 planar = sub(p, ld3(q.q));
+        u = dot(ld3(q.w), cross(planar, ld3(q.v)));
+        v = dot(ld3(q.w), cross(ld3(q.u), planar));
+        outward = ld3(q.normal);
+        h.mat = q.material;
+    } else {  // triangle
+        const gs_triangle& tr = sc.tris[idx];
+        double tt;
+        tri_hit(tr, r, tt, u, v);
+        p = add(r.o, muls(r.d, t));
+        outward = ld3(tr.normal);
+        h.mat = tr.material;
+    }
+    // HitRecord::new (hittable.rs:26-43)
+    h.front = dot(r.d, outward) < 0.0;
+    d3 n = h.front ? outward : neg(outward);
+    // Innermost instance first (RotateY inside Translate: rotate back, then translate).
+    if (nch > 3) inst_backward(sc.inst[ch3], p, n);
+    if (nch > 2) inst_backward(sc.inst[ch2], p, n);
+    if (nch > 1) inst_backward(sc.inst[ch1], p, n);
+    if (nch > 0) inst_backward(sc.inst[ch0], p, n);
+    h.p = p;
+    h.n = n;
+    h.u = u;
+    h.v = v;
+}
+
+// Texture::value_at (texture.rs:27-95); checkered nesting resolved iteratively.
+__device__ __noinline__ d3 texture_value(const DevScene& sc, uint32_t tex, double u, double v, d3 p,
+                                         unsigned long long* cnt) {
+#pragma unroll 1
+    for (int depth = 0; depth < 16; depth++) {
+        const gs_texture& t = sc.texs[tex];
+        if (t.kind == GS_TEX_SOLID) return ld3(t.color);
+        if (t.kind == GS_TEX_CHECKERED) {
+            int32_t xi = sat_i32(floor(t.scale_inv * p.x));
+            int32_t yi = sat_i32(floor(t.scale_inv * p.y));
+            int32_t zi = sat_i32(floor(t.scale_inv * p.z));
+            int32_t s = (int32_t)((uint32_t)xi + (uint32_t)yi + (uint32_t)zi);
+            tex = (s % 2 == 0) ? t.even : t.odd;
+            continue;
+        }
+        // GS_TEX_IMAGE
+        const gs_image im = sc.images[t.image];
+        double uc = u, vc = v;
+        if (uc < 0.0) uc = 0.0;
+        if (uc > 1.0) uc = 1.0;
+        if (vc < 0.0) vc = 0.0;
+        if (vc > 1.0) vc = 1.0;
+        vc = 1.0 - vc;
+        uint64_t i = sat_u64(uc * (double)im.width, 4294967295.0, 4294967295ull);
+        uint64_t j = sat_u64(vc * (double)im.height, 4294967295.0, 4294967295ull);
+        if (i > im.width - 1) i = im.width - 1;  // reference panics here (u == 1); documented clamp
+        if (j > im.height - 1) j = im.height - 1;
+        const uint8_t* px = sc.texels + im.offset + (j * (uint64_t)im.width + i) * 3;
+        atomicAdd(&cnt[C_IMG], 1ull);
+        return muls(mk((double)px[0], (double)px[1], (double)px[2]), 1.0 / 255.0);
+    }
+    return mk(0.0, 0.0, 0.0);
+}
+
+// Camera::sample_background / HDRI::sample (camera.rs:228-233, 257-270).
+__device__ __noinline__ d3 background(const DevScene& sc, d3 dir, unsigned long long* cnt) {
+    const gs_background& bg = sc.bg;
+    if (bg.kind == GS_BG_SOLID) return ld3(bg.color);
+    const double PI = 3.14159265358979323846;
+    d3 rv = mk(dir.x * bg.rot[0] + dir.y * bg.rot[1] + dir.z * bg.rot[2],
+               dir.x * bg.rot[3] + dir.y * bg.rot[4] + dir.z * bg.rot[5],
+               dir.x * bg.rot[6] + dir.y * bg.rot[7] + dir.z * bg.rot[8]);
+    d3 rot = unit(rv);
+    double theta = atan2(rot.y, rot.x);
+    double phi = asin(rot.z);
+    double u = 0.5 + theta / (2.0 * PI);
+    double v = 0.5 - phi / PI;
+    uint64_t x = sat_u64(u * (double)bg.width, 18446744073709551616.0, ~0ull) % (uint64_t)bg.width;
+    uint64_t y = sat_u64(v * (double)bg.height, 18446744073709551616.0, ~0ull) % (uint64_t)bg.height;
+    const float* px = sc.hdri + (y * (uint64_t)bg.width + x) * 3;
+    atomicAdd(&cnt[C_HDRI], 1ull);
+    return mk((double)px[0], (double)px[1], (double)px[2]);
+}
+
+__device__ __forceinline__ d3 random_unit_vector(uint64_t& rng) {  // util.rs:18-29
+    d3 v;
+#pragma unroll 1
+    for (;;) {
+        double x = wy_f64(rng) * 2.0 + -1.0;
+        double y = wy_f64(rng) * 2.0 + -1.0;
+        double z = wy_f64(rng) * 2.0 + -1.0;
+        v = mk(x, y, z);
+        if (len2(v) < 1.0) break;
+    }
+    return unit(v);
+}
+
+// Material::scatter (material.rs).  Returns false when the path ends (absorbed /
+// emitter); `att` and the new ray are set when it continues.  `emit` gets the
+// emitted colour (DiffuseLight only; every other material emits zero).
+__device__ __noinline__ bool scatter(const DevScene& sc, const HitRec& h, Ray& ray, uint64_t& rng, d3& att, d3& emit,
+                                     bool& emits, unsigned long long* cnt) {
+    const DMaterial& m = sc.mats[h.mat];
+    emits = false;
+    if (m.kind == GS_MAT_LAMBERTIAN) {  // :45-68
+        att = texture_value(sc, m.texture, h.u, h.v, h.p, cnt);
+        // OrthonormalBasis::new (ONB.rs:10-23)
+        d3 w = unit(h.n);
+        d3 a = fabs(w.x) > 0.9 ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);
+        d3 vv = unit(cross(w, a));
+        d3 uu = cross(w, vv);
+        // random_cosine_direction (util.rs:48-60), r2^(1/4) quirk kept
+        const double PI = 3.14159265358979323846;
+        double r1 = wy_f64(rng);
+        double r2 = wy_f64(rng);
+        double phi = 2.0 * PI * r1;
+        double r2s = sqrt(r2);
+        double sp, cp;
+        sincos(phi, &sp, &cp);
+        double q = sqrt(r2s);
+        d3 cd = mk(cp * q, sp * q, sqrt(1.0 - r2));
+        d3 dir = unit(add(add(muls(uu, cd.x), muls(vv, cd.y)), muls(w, cd.z)));
+        ray.o = h.p;
+        ray.d = dir;
+        return true;
+    }
+    if (m.kind == GS_MAT_METAL) {  // :87-102
+        d3 reflected = reflect(ray.d, h.n);
+        reflected = add(unit(reflected), muls(random_unit_vector(rng), m.param));
+        if (dot(reflected, h.n) > 0.0) {
+            att = ld3(m.albedo);
+            ray.o = h.p;
+            ray.d = reflected;
+            return true;
+        }
+        return false;
+    }
+    if (m.kind == GS_MAT_DIELECTRIC) {  // :123-148
+        double ri = h.front ? 1.0 / m.param : m.param;
+        d3 ud = unit(ray.d);
+        double cos_theta = fmin(dot(neg(ud), h.n), 1.0);
+        double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+        bool cannot_refract = ri * sin_theta > 1.0;
+        double r0 = (1.0 - ri) / (1.0 + ri);
+        r0 = r0 * r0;
+        double x = 1.0 - cos_theta;
+        double x2 = x * x;
+        double x4 = x2 * x2;
+        double refl = r0 + (1.0 - r0) * (x * x4);  // powi(x, 5) as LLVM expands it
+        bool fresnel = refl > wy_f64(rng);
+        d3 dir = (cannot_refract || fresnel) ? reflect(ud, h.n) : refract(ud, h.n, ri);
+        att = mk(1.0, 1.0, 1.0);
+        ray.o = h.p;
+        ray.d = dir;
+        return true;
+    }
+    if (m.kind == GS_MAT_DIFFUSE_LIGHT) {  // :165-169 (no scatter)
+        emit = texture_value(sc, m.texture, h.u, h.v, h.p, cnt);
+        emits = true;
+        return false;
+    }
+    return false;
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull << lane) - 1ull; }
+
+__global__ __launch_bounds__(GS_BLOCK) void gs_render_kernel(KArgs A) {
+    __shared__ uint32_t s_stack[GS_STACK * GS_BLOCK];
+    __shared__ unsigned long long s_cnt[C_N];
+    if (threadIdx.x < C_N) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+
+    const DevScene& sc = A.sc;
+    const gs_camera& cam = A.cam;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t tid = threadIdx.x;
+    const double tmin = 0.001;
+    const uint32_t tile_px = (uint32_t)(A.tile_w * A.tile_h);
+    const bool blocked8 = (A.tile_w % 8 == 0) && (A.tile_h % 8 == 0);
+    const double confidence_sq = A.ss.confidence * A.ss.confidence;
+    const double tolerance_sq = A.ss.tolerance * A.ss.tolerance;
+
+    uint32_t st = S_NEED;
+    bool qdone = false;
+
+    // pixel state
+    uint32_t item = 0, pix = 0, sample = 0, batch_left = 0;
+    int32_t pi = 0, pj = 0;
+    double scount = 0.0, csr = 0.0, csg = 0.0, csb = 0.0, lsum = 0.0, lsq = 0.0;
+    // path state
+    uint64_t rng = 0;
+    double Lr = 0, Lg = 0, Lb = 0, Tr = 1, Tg = 1, Tb = 1;
+    uint32_t depth = 0;
+    Ray ray;
+    ray.o = mk(0, 0, 0);
+    ray.d = mk(0, 0, 0);
+    ray.time = 0;
+    d3 inv = mk(0, 0, 0);
+    // traversal state
+    uint32_t cur = GS_REF_NONE, sp = 0, hit_ref = GS_REF_NONE, hit_inst = GS_REF_NONE;
+    double closest = 0.0;
+    // hot counters kept in registers, flushed per pixel
+    uint32_t c_nodes = 0, c_sph = 0;
+
+    auto begin_ray = [&]() {
+        inv = mk(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
+        cur = sc.root;
+        sp = 0;
+        closest = 1.7976931348623157e308;  // f64::MAX (camera.rs:177)
+        hit_ref = GS_REF_NONE;
+        hit_inst = GS_REF_NONE;
+        atomicAdd(&s_cnt[C_RAYS], 1ull);
+    };
+
+    // Start samples until one needs tracing or the pixel is finished.
+    // Returns with st = S_TRACE (ray ready) or S_NEED (pixel written).
+    auto next_sample = [&]() {
+#pragma unroll 1
+        for (;;) {
+            if (batch_left == 0) {
+                // end of a batch (camera.rs:149-164)
+                double mean = lsum / scount;
+                double variance_sq = 1.0 / (scount - 1.0) * (lsq - lsum * lsum / scount);
+                double convergence_sq = confidence_sq * variance_sq / scount;
+                bool stop = convergence_sq < (mean * mean * tolerance_sq);
+                if (!stop) stop = (uint32_t)sat_u64(scount, 4294967295.0, 4294967295ull) > A.ss.max_samples;
+                if (stop) {
+                    float* o = A.out + (size_t)item * 3;
+                    o[0] = (float)(csr / scount);
+                    o[1] = (float)(csg / scount);
+                    o[2] = (float)(csb / scount);
+                    atomicAdd(&s_cnt[C_PIX], 1ull);
+                    atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
+                    atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
+                    c_nodes = 0;
+                    c_sph = 0;
+                    st = S_NEED;
+                    return;
+                }
+                scount += (double)A.ss.batch_size;
+                batch_left = A.ss.batch_size;
+            }
+            // Camera::get_ray (camera.rs:204-221) on the seeded stream of this sample
+            rng = stream_seed(A.seed, pix, sample);
+            atomicAdd(&s_cnt[C_PATHS], 1ull);
+            double offx = wy_f64(rng) - 0.5;
+            double offy = wy_f64(rng) - 0.5;
+            double si = (double)pi + offx, sj = (double)pj + offy;
+            d3 ps = add(add(ld3(cam.starting_pixel_pos), muls(ld3(cam.pixel_delta_u), si)),
+                        muls(ld3(cam.pixel_delta_v), sj));
+            d3 org;
+            if (cam.defocus_angle <= 0.0) {
+                org = ld3(cam.center);
+            } else {  // defocus_disk_sample (camera.rs:223-226, util.rs:36-46)
+                double dx, dy;
+#pragma unroll 1
+                for (;;) {
+                    dx = wy_f64(rng) * 2.0 + -1.0;
+                    dy = wy_f64(rng) * 2.0 + -1.0;
+                    if (dx * dx + dy * dy + 0.0 * 0.0 < 1.0) break;
+                }
+                org = add(add(ld3(cam.center), muls(ld3(cam.defocus_disk_u), dx)), muls(ld3(cam.defocus_disk_v), dy));
+            }
+            ray.o = org;
+            ray.d = sub(ps, org);
+            ray.time = wy_f64(rng);
+            Lr = Lg = Lb = 0.0;
+            Tr = Tg = Tb = 1.0;
+            depth = cam.max_depth;
+            if (depth > 0) {
+                begin_ray();
+                st = S_TRACE;
+                return;
+            }
+            // ray_color(ray, 0) = 0: the sample contributes black (camera.rs:175)
+            sample++;
+            batch_left--;
+            // pixel_color += 0; lum = 0
+            lsum += 0.0;
+            lsq += 0.0;
+        }
+    };
+
+    auto end_path = [&]() {
+        // camera.rs:142-146
+        csr += Lr;
+        csg += Lg;
+        csb += Lb;
+        double lum = 0.299 * Lr + 0.587 * Lg + 0.144 * Lb;
+        lsum += lum;
+        lsq += lum * lum;
+        sample++;
+        batch_left--;
+        next_sample();
+    };
+
+#pragma unroll 1
+    for (;;) {
+        // ---------------------------------------------------------- refill
+        uint64_t need = __ballot(st == S_NEED);
+#pragma unroll 1
+        while (need != 0 && !qdone) {
+            const uint32_t n = (uint32_t)__popcll(need);
+            const uint32_t leader = (uint32_t)__ffsll((long long)need) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(A.queue, n);
+            base = __shfl(base, leader);
+            if ((uint64_t)base + n >= (uint64_t)A.capacity) qdone = true;
+            if (st == S_NEED) {
+                const uint64_t q = (uint64_t)base + (uint64_t)__popcll(need & lanemask_lt(lane));
+                if (q >= A.capacity) {
+                    st = S_DONE;
+                } else {
+                    // work order: 8x8 blocks inside each tile (coherent primary rays)
+                    const uint32_t slot = (uint32_t)(q / tile_px), w = (uint32_t)(q % tile_px);
+                    uint32_t x, y;
+                    if (blocked8) {
+                        const uint32_t b = w >> 6, l = w & 63, bpr = (uint32_t)A.tile_w >> 3;
+                        x = (b % bpr) * 8 + (l & 7);
+                        y = (b / bpr) * 8 + (l >> 3);
+                    } else {
+                        x = w % (uint32_t)A.tile_w;
+                        y = w / (uint32_t)A.tile_w;
+                    }
+                    item = slot * tile_px + y * (uint32_t)A.tile_w + x;
+                    const uint32_t tile = (uint32_t)A.rank + slot * (uint32_t)A.world_size;
+                    pi = (int32_t)((tile % (uint32_t)A.tiles_x) * (uint32_t)A.tile_w + x);
+                    pj = (int32_t)((tile / (uint32_t)A.tiles_x) * (uint32_t)A.tile_h + y);
+                    if (pi >= cam.image_width || pj >= cam.image_height) {
+                        float* o = A.out + (size_t)item * 3;  // padding pixel
+                        o[0] = 0.0f;
+                        o[1] = 0.0f;
+                        o[2] = 0.0f;
+                    } else {
+                        pix = (uint32_t)pj * (uint32_t)cam.image_width + (uint32_t)pi;
+                        sample = 0;
+                        batch_left = 0;
+                        scount = 0.0;
+                        csr = csg = csb = 0.0;
+                        lsum = lsq = 0.0;
+                        // first batch starts (camera.rs:137)
+                        scount += (double)A.ss.batch_size;
+                        batch_left = A.ss.batch_size;
+                        next_sample();
+                    }
+                }
+            }
+            need = __ballot(st == S_NEED);
+        }
+        if (st == S_NEED) st = S_DONE;
+        if (__ballot(st == S_TRACE || st == S_SHADE) == 0) break;
+
+        // ------------------------------------------------------- traverse
+#pragma unroll 1
+        for (;;) {
+            const uint64_t tr = __ballot(st == S_TRACE);
+            if (tr == 0) break;
+            if ((uint32_t)__popcll(__ballot(st == S_SHADE)) >= (uint32_t)A.shade_batch) break;
+            if (st == S_TRACE) {
+                const uint32_t kind = cur >> GS_REF_SHIFT;
+                if (kind == GS_REF_NODE) {
+                    const DNode nd = sc.nodes[cur & GS_REF_MASK];
+                    c_nodes++;
+                    if (box_hit(nd, ray.o, inv, tmin, closest)) {
+                        if (nd.right != GS_REF_NONE) {
+                            s_stack[sp * GS_BLOCK + tid] = nd.right;
+                            sp++;
+                        }
+                        cur = nd.left;
+                    } else {
+                        cur = GS_REF_NONE;
+                    }
+                } else {
+                    leaf_test(sc, cur, ray, tmin, closest, hit_ref, hit_inst, s_cnt, c_sph);
+                    cur = GS_REF_NONE;
+                }
+                if (cur == GS_REF_NONE) {
+                    if (sp > 0) {
+                        sp--;
+                        cur = s_stack[sp * GS_BLOCK + tid];
+                    } else {
+                        st = S_SHADE;
+                    }
+                }
+            }
+        }
+
+        // ---------------------------------------------------------- shade
+        if (st == S_SHADE) {
+            if (hit_ref == GS_REF_NONE) {
+                // miss: sample_background (camera.rs:201)
+                d3 bg = background(sc, ray.d, s_cnt);
+                Lr = Lr + Tr * bg.x;
+                Lg = Lg + Tg * bg.y;
+                Lb = Lb + Tb * bg.z;
+                end_path();
+            } else {
+                atomicAdd(&s_cnt[C_HITS], 1ull);
+                HitRec h;
+                reconstruct(sc, ray, closest, hit_ref, hit_inst, h);
+                d3 att = mk(0, 0, 0), emit = mk(0, 0, 0);
+                bool emits = false;
+                bool cont = scatter(sc, h, ray, rng, att, emit, emits, s_cnt);
+                if (emits) {
+                    Lr = Lr + Tr * emit.x;
+                    Lg = Lg + Tg * emit.y;
+                    Lb = Lb + Tb * emit.z;
+                }
+                if (cont) {
+                    Tr = Tr * att.x;
+                    Tg = Tg * att.y;
+                    Tb = Tb * att.z;
+                    depth--;
+                    if (depth > 0) {
+                        begin_ray();
+                        st = S_TRACE;
+                    } else {
+                        end_path();  // ray_color(.., 0) = 0 (camera.rs:175)
+                    }
+                } else {
+                    end_path();
+                }
+            }
+        }
+    }
+
+    // flush counters: LDS -> global, one atomic per counter per block
+    atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
+    atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
+    __syncthreads();
+    if (threadIdx.x < C_N && A.counters) atomicAdd(&A.counters[threadIdx.x], s_cnt[threadIdx.x]);
+}
+
+// Scatter rank-packed tiles into the frame.
+__global__ void gs_unpack_kernel(const float* __restrict__ in, float* __restrict__ frame, int32_t W, int32_t H,
+                                 int32_t world, int32_t tile_w, int32_t tile_h, int32_t tiles_x, uint64_t capacity) {
+    const uint64_t total = capacity * (uint64_t)world;
+    const uint32_t tile_px = (uint32_t)(tile_w * tile_h);
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total; g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = (uint32_t)(g / capacity);
+        const uint64_t k = g % capacity;
+        const uint32_t slot = (uint32_t)(k / tile_px), w = (uint32_t)(k % tile_px);
+        const uint32_t tile = r + slot * (uint32_t)world;
+        const int32_t x = (int32_t)((tile % (uint32_t)tiles_x) * (uint32_t)tile_w + w % (uint32_t)tile_w);
+        const int32_t y = (int32_t)((tile / (uint32_t)tiles_x) * (uint32_t)tile_h + w / (uint32_t)tile_w);
+        if (x < W && y < H) {
+            const size_t o = ((size_t)y * (size_t)W + (size_t)x) * 3;
+            frame[o] = in[g * 3];
+            frame[o + 1] = in[g * 3 + 1];
+            frame[o + 2] = in[g * 3 + 2];
+        }
+    }
+}
+
+// =============================================================== host side
+static thread_local std::string tl_err;
+static int32_t g_shade_batch = 32;
+static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
+
+extern "C" void gs_set_last_error(const char* msg) { tl_err = msg ? msg : ""; }
+static gs_status fail(gs_status code, const std::string& msg) {
+    tl_err = msg;
+    return code;
+}
+#define HIPCHK(x)                                                                               \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess) return fail(GS_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct gs_device_scene {
+    int device = 0;
+    void* mem = nullptr;  // one allocation for every array
+    size_t bytes = 0;
+    uint32_t* queue = nullptr;
+    DevScene dev{};
+    uint32_t n_nodes = 0;
+};
+
+namespace {
+
+struct Layout {
+    std::vector<uint8_t> blob;
+    size_t add(const void* p, size_t n) {
+        size_t off = (blob.size() + 255) & ~(size_t)255;
+        blob.resize(off + n + 1, 0);  // +1 keeps empty arrays at distinct, valid addresses
+        if (n && p) std::memcpy(blob.data() + off, p, n);
+        return off;
+    }
+};
+
+// Host-side validation of everything the kernel indexes, so a malformed scene is an
+// error code, never a GPU fault.
+gs_status validate(const gs_flat_scene& s) {
+    auto bad = [](const std::string& m) { return fail(GS_ERR_ARG, "invalid flat scene: " + m); };
+    auto unsup = [](const std::string& m) { return fail(GS_ERR_UNSUPPORTED, m); };
+    if (!s.nodes && s.n_nodes) return bad("nodes");
+    if (s.n_materials == 0 || !s.materials) return bad("no materials");
+    auto prim_ok = [&](uint32_t r) {
+        uint32_t k = r >> GS_REF_SHIFT, i = r & GS_REF_MASK;
+        switch (k) {
+            case GS_REF_SPHERE: return i < s.n_spheres;
+            case GS_REF_MSPHERE: return i < s.n_mspheres;
+            case GS_REF_QUAD: return i < s.n_quads;
+            case GS_REF_TRIANGLE: return i < s.n_triangles;
+            default: return false;
+        }
+    };
+    auto leaf_ok = [&](uint32_t r) -> int {  // 0 ok, 1 bad, 2 unsupported
+        uint32_t cur = r;
+        int chain = 0;
+        while ((cur >> GS_REF_SHIFT) == GS_REF_INSTANCE) {
+            uint32_t i = cur & GS_REF_MASK;
+            if (i >= s.n_instances) return 1;
+            if (++chain > GS_MAX_CHAIN) return 2;
+            const gs_instance& in = s.instances[i];
+            if (in.kind != GS_INST_TRANSLATE && in.kind != GS_INST_ROTATE_Y) return 1;
+            cur = in.child;
+        }
+        if ((cur >> GS_REF_SHIFT) == GS_REF_LIST) {
+            uint32_t i = cur & GS_REF_MASK;
+            if (i >= s.n_lists) return 1;
+            const gs_list& l = s.lists[i];
+            if ((uint64_t)l.first + l.count > s.n_list_refs) return 1;
+            for (uint32_t k = 0; k < l.count; k++)
+                if (!prim_ok(s.list_refs[l.first + k])) return 2;
+            return 0;
+        }
+        if ((cur >> GS_REF_SHIFT) == GS_REF_NODE) return chain ? 2 : 1;
+        return prim_ok(cur) ? 0 : 1;
+    };
+    // Walk the tree from the root: indices in range, no node reached twice, depth bound.
+    std::vector<uint8_t> seen(s.n_nodes, 0);
+    std::vector<std::pair<uint32_t, uint32_t>> stk;
+    stk.push_back({s.root, 0});
+    uint32_t maxd = 0;
+    while (!stk.empty()) {
+        auto [r, d] = stk.back();
+        stk.pop_back();
+        if ((r >> GS_REF_SHIFT) == GS_REF_NODE) {
+            uint32_t i = r & GS_REF_MASK;
+            if (i >= s.n_nodes) return bad("node index");
+            if (seen[i]) return bad("node reached twice (not a tree)");
+            seen[i] = 1;
+            if (d + 1 > maxd) maxd = d + 1;
+            if (s.nodes[i].left == GS_REF_NONE) return bad("node without left child");
+            stk.push_back({s.nodes[i].left, d + 1});
+            if (s.nodes[i].right != GS_REF_NONE) stk.push_back({s.nodes[i].right, d + 1});
+        } else {
+            int e = leaf_ok(r);
+            if (e == 1) return bad("leaf reference");
+            if (e == 2) return unsup("instance chain deeper than 4, BVH under an instance, or a list member "
+                                     "that is not a primitive");
+        }
+    }
+    if (maxd > GS_STACK) return unsup("BVH deeper than the device stack (" + std::to_string(GS_STACK) + ")");
+    auto mat_ok = [&](uint32_t m) { return m < s.n_materials; };
+    for (uint32_t i = 0; i < s.n_spheres; i++) if (!mat_ok(s.spheres[i].material)) return bad("sphere material");
+    for (uint32_t i = 0; i < s.n_mspheres; i++) if (!mat_ok(s.mspheres[i].material)) return bad("msphere material");
+    for (uint32_t i = 0; i < s.n_quads; i++) if (!mat_ok(s.quads[i].material)) return bad("quad material");
+    for (uint32_t i = 0; i < s.n_triangles; i++) if (!mat_ok(s.triangles[i].material)) return bad("triangle material");
+    for (uint32_t i = 0; i < s.n_materials; i++) {
+        const gs_material& m = s.materials[i];
+        if (m.kind == GS_MAT_LAMBERTIAN || m.kind == GS_MAT_DIFFUSE_LIGHT) {
+            if (m.texture >= s.n_textures) return bad("material texture");
+        } else if (m.kind == GS_MAT_ISOTROPIC) {
+            return unsup("Isotropic material (volumes) on the device path");
+        } else if (m.kind != GS_MAT_METAL && m.kind != GS_MAT_DIELECTRIC) {
+            return bad("material kind");
+        }
+    }
+    for (uint32_t i = 0; i < s.n_textures; i++) {
+        const gs_texture& t = s.textures[i];
+        if (t.kind == GS_TEX_CHECKERED) {
+            if (t.even >= s.n_textures || t.odd >= s.n_textures) return bad("checkered child");
+        } else if (t.kind == GS_TEX_IMAGE) {
+            if (t.image >= s.n_images) return bad("image index");
+            const gs_image& im = s.images[t.image];
+            if (!im.width || !im.height) return bad("empty image");
+            if (im.offset + (uint64_t)im.width * im.height * 3 > s.n_texels8) return bad("image texels out of range");
+        } else if (t.kind != GS_TEX_SOLID) {
+            return bad("texture kind");
+        }
+    }
+    if (s.background.kind == GS_BG_HDRI) {
+        if (!s.background.width || !s.background.height) return bad("empty HDRI");
+        if ((uint64_t)s.background.width * s.background.height * 3 > s.n_hdri_floats || !s.hdri_rgb)
+            return bad("HDRI texels");
+    } else if (s.background.kind != GS_BG_SOLID) {
+        return bad("background kind");
+    }
+    return GS_OK;
+}
+
+// Does the texture tree under `t` contain an image (=> sphere uv must be computed)?
+bool tex_needs_uv(const gs_flat_scene& s, uint32_t t, int depth = 0) {
+    if (t >= s.n_textures || depth > 16) return false;
+    const gs_texture& x = s.textures[t];
+    if (x.kind == GS_TEX_IMAGE) return true;
+    if (x.kind == GS_TEX_CHECKERED) return tex_needs_uv(s, x.even, depth + 1) || tex_needs_uv(s, x.odd, depth + 1);
+    return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gs_last_error(void) { return tl_err.c_str(); }
+int32_t gs_version(void) { return GS_ABI_VERSION; }
+
+gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu) {
+    if (shade_batch < 1 || shade_batch > 64 || blocks_per_cu < 0 || blocks_per_cu > 8)
+        return fail(GS_ERR_ARG, "bad tuning");
+    g_shade_batch = shade_batch;
+    g_blocks_per_cu = blocks_per_cu;
+    return GS_OK;
+}
+
+gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) {
+    if (!s || !out) return fail(GS_ERR_ARG, "null argument");
+    *out = nullptr;
+    gs_status v = validate(*s);
+    if (v != GS_OK) return v;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GS_ERR_NO_DEVICE, "no HIP device visible");
+
+    std::vector<DNode> nodes(s->n_nodes);
+    for (uint32_t i = 0; i < s->n_nodes; i++) {
+        const gs_node& n = s->nodes[i];
+        nodes[i] = DNode{n.min[0], n.min[1], n.min[2], n.max[0], n.max[1], n.max[2], n.left, n.right, 0, 0};
+    }
+    std::vector<DSphere> sph(s->n_spheres);
+    std::vector<uint32_t> sph_mat(s->n_spheres);
+    for (uint32_t i = 0; i < s->n_spheres; i++) {
+        const gs_sphere& x = s->spheres[i];
+        sph[i] = DSphere{x.center[0], x.center[1], x.center[2], x.radius};
+        sph_mat[i] = x.material;
+    }
+    std::vector<DMaterial> mats(s->n_materials);
+    for (uint32_t i = 0; i < s->n_materials; i++) {
+        const gs_material& m = s->materials[i];
+        DMaterial d{};
+        d.kind = m.kind;
+        d.texture = m.texture;
+        d.needs_uv = (m.kind == GS_MAT_LAMBERTIAN || m.kind == GS_MAT_DIFFUSE_LIGHT) ? tex_needs_uv(*s, m.texture) : 0;
+        for (int k = 0; k < 3; k++) d.albedo[k] = m.albedo[k];
+        d.param = m.param;
+        mats[i] = d;
+    }
+    Layout L;
+    size_t o_nodes = L.add(nodes.data(), nodes.size() * sizeof(DNode));
+    size_t o_sph = L.add(sph.data(), sph.size() * sizeof(DSphere));
+    size_t o_sphm = L.add(sph_mat.data(), sph_mat.size() * 4);
+    size_t o_msph = L.add(s->mspheres, s->n_mspheres * sizeof(gs_msphere));
+    size_t o_quad = L.add(s->quads, s->n_quads * sizeof(gs_quad));
+    size_t o_tri = L.add(s->triangles, s->n_triangles * sizeof(gs_triangle));
+    size_t o_list = L.add(s->lists, s->n_lists * sizeof(gs_list));
+    size_t o_lref = L.add(s->list_refs, s->n_list_refs * 4);
+    size_t o_inst = L.add(s->instances, s->n_instances * sizeof(gs_instance));
+    size_t o_mat = L.add(mats.data(), mats.size() * sizeof(DMaterial));
+    size_t o_tex = L.add(s->textures, s->n_textures * sizeof(gs_texture));
+    size_t o_img = L.add(s->images, s->n_images * sizeof(gs_image));
+    size_t o_texel = L.add(s->texels8, s->n_texels8);
+    size_t o_hdri = L.add(s->hdri_rgb, s->background.kind == GS_BG_HDRI ? s->n_hdri_floats * 4 : 0);
+    size_t o_queue = L.add(nullptr, 64);
+
+    auto ds = new gs_device_scene();
+    (void)hipGetDevice(&ds->device);
+    ds->bytes = L.blob.size();
+    if (hipMalloc(&ds->mem, ds->bytes) != hipSuccess) {
+        delete ds;
+        return fail(GS_ERR_OOM, "hipMalloc of " + std::to_string(L.blob.size()) + " bytes failed");
+    }
+    hipError_t e = hipMemcpy(ds->mem, L.blob.data(), ds->bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(ds->mem);
+        delete ds;
+        return fail(GS_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+    }
+    uint8_t* b = (uint8_t*)ds->mem;
+    DevScene& d = ds->dev;
+    d.nodes = (const DNode*)(b + o_nodes);
+    d.spheres = (const DSphere*)(b + o_sph);
+    d.sphere_mat = (const uint32_t*)(b + o_sphm);
+    d.mspheres = (const gs_msphere*)(b + o_msph);
+    d.quads = (const gs_quad*)(b + o_quad);
+    d.tris = (const gs_triangle*)(b + o_tri);
+    d.lists = (const gs_list*)(b + o_list);
+    d.list_refs = (const uint32_t*)(b + o_lref);
+    d.inst = (const gs_instance*)(b + o_inst);
+    d.mats = (const DMaterial*)(b + o_mat);
+    d.texs = (const gs_texture*)(b + o_tex);
+    d.images = (const gs_image*)(b + o_img);
+    d.texels = (const uint8_t*)(b + o_texel);
+    d.hdri = (const float*)(b + o_hdri);
+    d.bg = s->background;
+    d.root = s->root;
+    ds->queue = (uint32_t*)(b + o_queue);
+    ds->n_nodes = s->n_nodes;
+    *out = ds;
+    return GS_OK;
+}
+
+gs_status gs_device_scene_destroy(gs_device_scene* ds) {
+    if (!ds) return GS_OK;
+    if (ds->mem) (void)hipFree(ds->mem);
+    delete ds;
+    return GS_OK;
+}
+
+static bool part_ok(const gs_camera* cam, const gs_partition* p) {
+    return cam && p && cam->image_width > 0 && cam->image_height > 0 && p->world_size >= 1 && p->rank >= 0 &&
+           p->rank < p->world_size && p->tile_w > 0 && p->tile_h > 0 && (int64_t)p->tile_w * p->tile_h <= (1 << 20);
+}
+
+int64_t gs_partition_capacity(const gs_camera* cam, const gs_partition* p) {
+    if (!part_ok(cam, p)) return -1;
+    int64_t tx = (cam->image_width + p->tile_w - 1) / p->tile_w;
+    int64_t ty = (cam->image_height + p->tile_h - 1) / p->tile_h;
+    int64_t nt = tx * ty;
+    int64_t mine = nt > p->rank ? (nt - p->rank + p->world_size - 1) / p->world_size : 0;
+    return mine * p->tile_w * p->tile_h;
+}
+
+gs_status gs_render_tiles_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
+                                uint64_t seed, const gs_partition* part, float* d_out, gs_counters* d_counters,
+                                void* stream) {
+    if (!ds || !cam || !ss || !part || !d_out) return fail(GS_ERR_ARG, "null argument");
+    if (!part_ok(cam, part)) return fail(GS_ERR_ARG, "bad partition / image size");
+    if (ss->batch_size == 0) return fail(GS_ERR_ARG, "batch_size 0 never terminates (camera.rs:137)");
+    int64_t cap = gs_partition_capacity(cam, part);
+    if (cap <= 0) return GS_OK;
+    if (cap >= (int64_t)0xFFFFFFFFll) return fail(GS_ERR_ARG, "partition too large");
+    if ((int64_t)cam->image_width * cam->image_height >= (int64_t)0xFFFFFFFFll)
+        return fail(GS_ERR_ARG, "image too large for 32-bit pixel ids");
+    hipStream_t st = (hipStream_t)stream;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    if (dev != ds->device) return fail(GS_ERR_ARG, "scene lives on another device");
+    KArgs a{};
+    a.sc = ds->dev;
+    a.cam = *cam;
+    a.ss = *ss;
+    a.seed = seed;
+    a.rank = part->rank;
+    a.world_size = part->world_size;
+    a.tile_w = part->tile_w;
+    a.tile_h = part->tile_h;
+    a.tiles_x = (cam->image_width + part->tile_w - 1) / part->tile_w;
+    a.shade_batch = g_shade_batch;
+    a.capacity = (uint32_t)cap;
+    a.out = d_out;
+    a.counters = (unsigned long long*)d_counters;
+    a.queue = ds->queue;
+    HIPCHK(hipMemsetAsync(ds->queue, 0, 4, st));
+    int cus = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    int per_cu = g_blocks_per_cu;
+    if (per_cu <= 0) {
+        int occ = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gs_render_kernel, GS_BLOCK, 0));
+        per_cu = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
+    }
+    int64_t blocks = (int64_t)cus * per_cu;
+    // no more waves than work: one lane per pixel at most
+    int64_t max_blocks = (cap + GS_BLOCK - 1) / GS_BLOCK;
+    if (blocks > max_blocks) blocks = max_blocks;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(gs_render_kernel, dim3((unsigned)blocks), dim3(GS_BLOCK), 0, st, a);
+    HIPCHK(hipGetLastError());
+    return GS_OK;
+}
+
+gs_status gs_unpack_tiles_async(const gs_camera* cam, int32_t world_size, int32_t tile_w, int32_t tile_h,
+                                int64_t capacity, const float* d_in, float* d_frame, void* stream) {
+    gs_partition p{0, world_size, tile_w, tile_h};
+    if (!part_ok(cam, &p) || !d_in || !d_frame || capacity < 0) return fail(GS_ERR_ARG, "bad argument");
+    if (capacity % ((int64_t)tile_w * tile_h) != 0) return fail(GS_ERR_ARG, "capacity is not whole tiles");
+    if (capacity == 0) return GS_OK;
+    int32_t tiles_x = (cam->image_width + tile_w - 1) / tile_w;
+    uint64_t total = (uint64_t)capacity * world_size;
+    unsigned grid = (unsigned)std::min<uint64_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(gs_unpack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_in, d_frame,
+                       cam->image_width, cam->image_height, world_size, tile_w, tile_h, tiles_x, (uint64_t)capacity);
+    HIPCHK(hipGetLastError());
+    return GS_OK;
+}
+
+gs_status gs_render(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
+                    float* out_rgb, gs_counters* counters) {
+    if (!scene || !cam || !ss || !out_rgb) return fail(GS_ERR_ARG, "null argument");
+    gs_device_scene* ds = nullptr;
+    gs_status r = gs_device_scene_create(scene, &ds);
+    if (r != GS_OK) return r;
+    gs_partition p{0, 1, 64, 64};
+    int64_t cap = gs_partition_capacity(cam, &p);
+    if (cap < 0) {
+        gs_device_scene_destroy(ds);
+        return fail(GS_ERR_ARG, "bad image size");
+    }
+    const size_t W = (size_t)cam->image_width, H = (size_t)cam->image_height;
+    float *d_pack = nullptr, *d_frame = nullptr;
+    gs_counters* d_cnt = nullptr;
+    auto cleanup = [&]() {
+        if (d_pack) (void)hipFree(d_pack);
+        if (d_frame) (void)hipFree(d_frame);
+        if (d_cnt) (void)hipFree(d_cnt);
+        gs_device_scene_destroy(ds);
+    };
+    if (hipMalloc(&d_pack, (size_t)cap * 12 + 16) != hipSuccess || hipMalloc(&d_frame, W * H * 12 + 16) != hipSuccess ||
+        hipMalloc(&d_cnt, sizeof(gs_counters)) != hipSuccess) {
+        cleanup();
+        return fail(GS_ERR_OOM, "hipMalloc failed");
+    }
+    hipError_t e = hipMemset(d_cnt, 0, sizeof(gs_counters));
+    if (e == hipSuccess) e = hipMemset(d_frame, 0, W * H * 12);
+    if (e != hipSuccess) {
+        cleanup();
+        return fail(GS_ERR_HIP, hipGetErrorString(e));
+    }
+    r = gs_render_tiles_async(ds, cam, ss, seed, &p, d_pack, d_cnt, nullptr);
+    if (r == GS_OK) r = gs_unpack_tiles_async(cam, 1, p.tile_w, p.tile_h, cap, d_pack, d_frame, nullptr);
+    if (r == GS_OK) {
+        e = hipDeviceSynchronize();
+        if (e == hipSuccess) e = hipMemcpy(out_rgb, d_frame, W * H * 12, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && counters) e = hipMemcpy(counters, d_cnt, sizeof(gs_counters), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) r = fail(GS_ERR_HIP, hipGetErrorString(e));
+    }
+    cleanup();
+    return r;
+}
+
+}  // extern "C"

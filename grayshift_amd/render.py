@@ -1,0 +1,110 @@
+"""Python entry points to the device path (libgrayshift.so, HIP for gfx950).
+
+* ``render(scene)`` — the one-call ``Camera::render`` replacement (linear f32 frame).
+* ``Renderer`` — device-resident scene for repeated / multi-GPU rendering: upload once,
+  render this rank's tiles into a caller-provided device buffer on a given stream.
+  Used by bench.py with torch tensors as the device buffers (torch is plumbing only).
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+
+
+def camera(cam_spec):
+    """Camera::new (camera.rs:39-98) -> gs_camera (the fields the device reads)."""
+    out = N.gs_camera()
+    N.check(N.lib.gs_host_camera(C.byref(cam_spec), C.byref(out)))
+    return out
+
+
+def render(scene, seed=1):
+    """Render a scenes.Scene on the current HIP device.  Returns (rgb [H,W,3] f32, counters)."""
+    cam = camera(scene.camera)
+    out = np.zeros((cam.image_height, cam.image_width, 3), dtype=np.float32)
+    cnt = N.gs_counters()
+    N.check(N.lib.gs_host_render_spec(scene.spec.ptr(), C.byref(scene.camera), C.byref(scene.settings), seed,
+                                      out.ctypes.data, C.byref(cnt)))
+    return out, cnt.as_dict()
+
+
+def set_tuning(shade_batch=32, blocks_per_cu=0):
+    N.check(N.lib.gs_set_tuning(shade_batch, blocks_per_cu))
+
+
+def write_ppm(path, rgb):
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    N.check(N.lib.gs_host_write_ppm(path.encode(), rgb.shape[1], rgb.shape[0], rgb.ctypes.data))
+
+
+class HostScene:
+    """World + BVHNode::from_list + flat arrays, built by the C++ host mirror."""
+
+    def __init__(self, spec):
+        self._spec = spec
+        h = C.c_void_p()
+        N.check(N.lib.gs_host_scene_from_spec(spec.ptr(), C.byref(h)))
+        self.handle = h
+        self.flat_ptr = N.lib.gs_host_scene_flat(h)
+        self.flat = N.gs_flat_scene.from_address(self.flat_ptr)
+
+    def close(self):
+        if self.handle:
+            N.lib.gs_host_scene_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+    def stats(self):
+        f = self.flat
+        return {"nodes": f.n_nodes, "spheres": f.n_spheres, "mspheres": f.n_mspheres, "quads": f.n_quads,
+                "triangles": f.n_triangles, "lists": f.n_lists, "instances": f.n_instances,
+                "materials": f.n_materials, "textures": f.n_textures, "max_bvh_depth": f.max_bvh_depth}
+
+
+class Renderer:
+    """A scene resident in HBM of the current device, rendered tile-partitioned."""
+
+    def __init__(self, scene, rank=0, world_size=1, tile=64):
+        self.scene = scene
+        self.host = HostScene(scene.spec)
+        self.cam = camera(scene.camera)
+        self.settings = scene.settings
+        self.part = N.gs_partition(rank=rank, world_size=world_size, tile_w=tile, tile_h=tile)
+        self.capacity = N.lib.gs_partition_capacity(C.byref(self.cam), C.byref(self.part))
+        if self.capacity < 0:
+            raise ValueError("bad partition")
+        d = C.c_void_p()
+        N.check(N.lib.gs_device_scene_create(self.host.flat_ptr, C.byref(d)))
+        self.dev = d
+
+    @property
+    def width(self):
+        return self.cam.image_width
+
+    @property
+    def height(self):
+        return self.cam.image_height
+
+    def render_async(self, d_packed, d_counters=0, stream=0, seed=1):
+        """d_packed: device pointer to capacity*3 f32; d_counters: device gs_counters or 0."""
+        N.check(N.lib.gs_render_tiles_async(self.dev, C.byref(self.cam), C.byref(self.settings), seed,
+                                            C.byref(self.part), C.c_void_p(d_packed), C.c_void_p(d_counters),
+                                            C.c_void_p(stream)))
+
+    def unpack_async(self, d_gathered, d_frame, world_size, stream=0):
+        N.check(N.lib.gs_unpack_tiles_async(C.byref(self.cam), world_size, self.part.tile_w, self.part.tile_h,
+                                            self.capacity, C.c_void_p(d_gathered), C.c_void_p(d_frame),
+                                            C.c_void_p(stream)))
+
+    def close(self):
+        if getattr(self, "dev", None):
+            N.lib.gs_device_scene_destroy(self.dev)
+            self.dev = None
+        if getattr(self, "host", None):
+            self.host.close()
+
+    def __del__(self):
+        self.close()

@@ -1,0 +1,229 @@
+/*
+ * grayshift_gpu.h — the C-ABI drop-in boundary of the MI355X path tracer.
+ *
+ * This is what the reference's `Camera::render` (src/camera.rs:100) calls in place
+ * of its pixel loop (camera.rs:105-114: pixel list + rayon `par_iter` + `sample`).
+ * The host (the reference's Rust crate, or the C++ mirror in grayshift_amd/csrc/host)
+ * builds the world, builds the BVH with the reference's own median split
+ * (hittable/BVH.rs:18-65) and flattens it into the plain arrays below; the library
+ * copies them into HBM and runs the persistent HIP megakernel.  The output stage
+ * (PPM header + write_color, camera.rs:101-103,116-118) stays on the host.
+ *
+ * Plain pointers and sizes only; no torch, no HIP types in the signatures (a stream
+ * is passed as `void*`).  No exceptions cross the ABI: every entry point returns a
+ * gs_status and leaves a message for gs_last_error().  Not reentrant on the same
+ * gs_device_scene; reentrant on distinct scenes/devices.
+ */
+#ifndef GRAYSHIFT_GPU_H
+#define GRAYSHIFT_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "grayshift_scene.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_ABI_VERSION 1
+
+typedef int32_t gs_status;
+enum {
+    GS_OK = 0,
+    GS_ERR_ARG = -1,         /* bad argument / malformed scene */
+    GS_ERR_HIP = -2,         /* HIP runtime error */
+    GS_ERR_OOM = -3,         /* device allocation failed */
+    GS_ERR_UNSUPPORTED = -4, /* scene feature the device path does not implement */
+    GS_ERR_NO_DEVICE = -5    /* no gfx950 device visible */
+};
+
+/* ---- tagged child references (32 bit: kind << 28 | index) ---- */
+#define GS_REF_SHIFT 28u
+#define GS_REF_MASK 0x0FFFFFFFu
+enum gs_ref_kind {
+    GS_REF_NONE = 0,     /* absent right child (BVH.rs:20-28 n == 1 wrapper) */
+    GS_REF_NODE = 1,     /* BVHNode                       -> nodes[]     */
+    GS_REF_SPHERE = 2,   /* stationary Sphere             -> spheres[]   */
+    GS_REF_MSPHERE = 3,  /* moving Sphere                 -> mspheres[]  */
+    GS_REF_QUAD = 4,     /* Quad                          -> quads[]     */
+    GS_REF_TRIANGLE = 5, /* Triangle                      -> triangles[] */
+    GS_REF_LIST = 6,     /* HittableList of primitives    -> lists[]     */
+    GS_REF_INSTANCE = 7  /* Translate / RotateY           -> instances[] */
+};
+#define GS_MAKE_REF(kind, idx) (((uint32_t)(kind) << GS_REF_SHIFT) | ((uint32_t)(idx) & GS_REF_MASK))
+
+/* BVH node: the reference AABB in f64 (AABB.rs:7-11) and the two children.
+ * 64 B = one cache line, array-of-structs: a lane reads its whole node at once. */
+typedef struct gs_node {
+    double min[3];
+    double max[3];
+    uint32_t left, right; /* tagged refs; right may be GS_REF_NONE */
+    uint32_t pad[2];
+} gs_node;
+
+/* Stationary sphere (sphere.rs:11-18): 40 B. */
+typedef struct gs_sphere {
+    double center[3];
+    double radius;
+    uint32_t material;
+    uint32_t pad;
+} gs_sphere;
+
+/* Moving sphere: center(time) = center_start + time * center_path (sphere.rs:51-53). 64 B. */
+typedef struct gs_msphere {
+    double center_start[3];
+    double center_path[3];
+    double radius;
+    uint32_t material;
+    uint32_t pad;
+} gs_msphere;
+
+/* Quad with its plane (quad.rs:12-38, plane.rs:10-18): 136 B. */
+typedef struct gs_quad {
+    double q[3], u[3], v[3], w[3];
+    double normal[3];
+    double d;
+    uint32_t material;
+    uint32_t pad;
+} gs_quad;
+
+/* Triangle (triangle.rs:10-28): normal = (b-a)x(c-a), unnormalised. 104 B. */
+typedef struct gs_triangle {
+    double a[3], b[3], c[3];
+    double normal[3];
+    uint32_t material;
+    uint32_t pad;
+} gs_triangle;
+
+/* HittableList (hittable.rs:45-91): list_refs[first .. first+count), each a primitive ref. */
+typedef struct gs_list {
+    uint32_t first, count;
+} gs_list;
+
+/* Instance transform, one per Translate / RotateY (hittable.rs:93-215). 32 B.
+ * child: the wrapped object (another instance, a list or a primitive). */
+enum { GS_INST_TRANSLATE = 1, GS_INST_ROTATE_Y = 2 };
+typedef struct gs_instance {
+    uint32_t kind;
+    uint32_t child;
+    double p[3]; /* TRANSLATE: offset; ROTATE_Y: sin_theta, cos_theta, 0 */
+} gs_instance;
+
+/* Material record (material.rs): 40 B. */
+typedef struct gs_material {
+    uint32_t kind;    /* gs_mat_kind */
+    uint32_t texture; /* LAMBERTIAN / DIFFUSE_LIGHT */
+    double albedo[3]; /* METAL */
+    double param;     /* METAL: fuzz; DIELECTRIC: refraction_index */
+} gs_material;
+
+/* Texture record (texture.rs): 48 B. */
+typedef struct gs_texture {
+    uint32_t kind;      /* gs_tex_kind */
+    uint32_t even, odd; /* CHECKERED: texture indices */
+    uint32_t image;     /* IMAGE: index into images[] */
+    double color[3];    /* SOLID */
+    double scale_inv;   /* CHECKERED: 1/scale (texture.rs:42) */
+} gs_texture;
+
+typedef struct gs_image {
+    uint32_t width, height;
+    uint64_t offset; /* byte offset into texels8 (RGB8, row-major, top row first) */
+} gs_image;
+
+/* Background (camera.rs:246-270).  For HDRI the rotation's matrix entries are
+ * precomputed by the host with the exact expressions of rotate_vector (util.rs:67-86). */
+typedef struct gs_background {
+    uint32_t kind; /* gs_bg_kind */
+    uint32_t width, height;
+    uint32_t pad;
+    double color[3];
+    double rot[9]; /* row-major: x' = v.x*rot[0] + v.y*rot[1] + v.z*rot[2], ... */
+} gs_background;
+
+/* Flattened scene as handed over by the host. */
+typedef struct gs_flat_scene {
+    uint32_t root; /* tagged ref of the world BVH root */
+    uint32_t max_bvh_depth;
+    const gs_node* nodes;         uint32_t n_nodes;
+    const gs_sphere* spheres;     uint32_t n_spheres;
+    const gs_msphere* mspheres;   uint32_t n_mspheres;
+    const gs_quad* quads;         uint32_t n_quads;
+    const gs_triangle* triangles; uint32_t n_triangles;
+    const gs_list* lists;         uint32_t n_lists;
+    const uint32_t* list_refs;    uint32_t n_list_refs;
+    const gs_instance* instances; uint32_t n_instances;
+    const gs_material* materials; uint32_t n_materials;
+    const gs_texture* textures;   uint32_t n_textures;
+    const gs_image* images;       uint32_t n_images;
+    const uint8_t* texels8;       uint64_t n_texels8;  /* bytes */
+    gs_background background;
+    const float* hdri_rgb;        uint64_t n_hdri_floats; /* width*height*3 */
+} gs_flat_scene;
+
+/* The fields `Camera::new` derives (camera.rs:17-98), computed by the host. */
+typedef struct gs_camera {
+    int32_t image_width, image_height;
+    uint32_t max_depth;
+    uint32_t pad;
+    double center[3];
+    double starting_pixel_pos[3];
+    double pixel_delta_u[3];
+    double pixel_delta_v[3];
+    double defocus_angle;
+    double defocus_disk_u[3];
+    double defocus_disk_v[3];
+} gs_camera;
+
+/* Image-space partition: the frame is cut into tile_w x tile_h tiles, tile k goes
+ * to rank k mod world_size (round-robin, for load balance under adaptive sampling).
+ * A rank's pixels are packed tile after tile, each tile row-major inside, padded to
+ * full tiles: packed index = slot*tile_w*tile_h + ty*tile_w + tx. */
+typedef struct gs_partition {
+    int32_t rank, world_size;
+    int32_t tile_w, tile_h;
+} gs_partition;
+
+/* Device-resident scene (opaque): uploaded once, rendered many times. */
+typedef struct gs_device_scene gs_device_scene;
+
+const char* gs_last_error(void);
+int32_t gs_version(void);
+
+/* Launch tuning, process-wide: shade_batch in [1, 64] = finished lanes a wave
+ * collects before it shades them together; blocks_per_cu in [0, 8], 0 = from the
+ * occupancy query. */
+gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu);
+
+/* Upload a flattened scene to the current HIP device. */
+gs_status gs_device_scene_create(const gs_flat_scene* scene, gs_device_scene** out);
+gs_status gs_device_scene_destroy(gs_device_scene* scene);
+
+/* Number of packed pixels (tiles * tile_w * tile_h) this rank renders. */
+int64_t gs_partition_capacity(const gs_camera* cam, const gs_partition* part);
+
+/* Render this rank's tiles asynchronously on `stream` (hipStream_t as void*, NULL =
+ * default stream).  d_packed_rgb: device buffer of capacity*3 f32, linear colour
+ * (pixel_color / sample_count, camera.rs:167) for each packed pixel; padding pixels
+ * are written as 0.  d_counters: device gs_counters (nullable), accumulated into. */
+gs_status gs_render_tiles_async(const gs_device_scene* scene, const gs_camera* cam,
+                                const gs_sample_settings* ss, uint64_t seed,
+                                const gs_partition* part, float* d_packed_rgb,
+                                gs_counters* d_counters, void* stream);
+
+/* Scatter the packed buffers of all ranks (world_size * capacity * 3 f32, rank-major,
+ * as a gather leaves them) into a W*H*3 frame.  Runs on the current device. */
+gs_status gs_unpack_tiles_async(const gs_camera* cam, int32_t world_size, int32_t tile_w,
+                                int32_t tile_h, int64_t capacity, const float* d_gathered,
+                                float* d_frame, void* stream);
+
+/* Synchronous full-frame render on the current device: upload, render, copy back.
+ * out_rgb: host buffer W*H*3 f32 (linear).  counters: host, nullable.  This is the
+ * one-call replacement for camera.rs:105-114. */
+gs_status gs_render(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss,
+                    uint64_t seed, float* out_rgb, gs_counters* counters);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GRAYSHIFT_GPU_H */
