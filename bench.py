@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s (primary + secondary rays) of the MI355X megakernel.
+
+Contract:
+    python bench.py --gpus N --steps K --warmup W
+One step = one full frame of the configured workload (default C4: the 10k-sphere
+BVH scene, 1920x1080, 512 spp, HDRI sky), tile-partitioned round-robin over the N
+ranks (64x64 tiles), then one RCCL gather of the finished tiles to rank 0 and an
+unpack into the frame.  The scene is resident in HBM before timing starts.
+value = all rays traced by all ranks / wall time (max over ranks); a "ray" is one
+world.hit call (camera.rs:177), counted on the device by the very launches timed.
+
+Rank 0 prints ONE JSON line.  At N=1, rank 0 also times the CPU oracle (the
+reference's algorithm restated in C++, oracle/) on a bounded 1/64 pixel subset
+of the same frame: `cpu_baseline`.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Algorithmic bytes per unit: what the reference
+# algorithm reads for each counted event.
+BYTES = {"node_visits": 56, "sphere_tests": 40, "msphere_tests": 64, "quad_tests": 136, "tri_tests": 104,
+         "instance_tests": 32, "hits": 32, "image_texels": 3, "hdri_texels": 12, "pixels": 12}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(c):
+    return sum(BYTES[k] * int(c[k]) for k in BYTES)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C4", help="BASELINE config C1..C5 (default C4)")
+    ap.add_argument("--width", type=int, default=None, help="override (testing only; invalidates the metric)")
+    ap.add_argument("--spp", type=int, default=None, help="override (testing only; invalidates the metric)")
+    ap.add_argument("--tile", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--shade-batch", type=int, default=None)
+    ap.add_argument("--blocks-per-cu", type=int, default=None)
+    ap.add_argument("--cpu-stride", type=int, default=4, help="CPU baseline: every Nth row and column")
+    ap.add_argument("--cpu-threads", type=int, default=None)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch (profiles/)")
+    ap.add_argument("--dump", default=None, help="write the frame (rank 0) as .npy")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus %d needs torch.distributed.run with %d ranks" % (a.gpus, a.gpus))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import grayshift_amd as g
+    from grayshift_amd import scenes
+
+    if a.shade_batch is not None or a.blocks_per_cu is not None:
+        g.set_tuning(a.shade_batch or 32, a.blocks_per_cu or 0)
+    sc = scenes.config(a.config, width=a.width, spp=a.spp)
+    r = g.Renderer(sc, rank=rank, world_size=world, tile=a.tile)
+    # Every rank's packed buffer has rank 0's capacity (round-robin gives it the most tiles)
+    cap0 = g._native.lib.gs_partition_capacity(
+        __import__("ctypes").byref(r.cam),
+        __import__("ctypes").byref(g._native.gs_partition(0, world, a.tile, a.tile)))
+    dev = torch.device("cuda", local)
+    packed = torch.zeros(cap0 * 3, dtype=torch.float32, device=dev)
+    counters = torch.zeros(16, dtype=torch.int64, device=dev)
+    frame = torch.zeros(r.height * r.width * 3, dtype=torch.float32, device=dev) if rank == 0 else None
+    gathered = torch.empty(world * cap0 * 3, dtype=torch.float32, device=dev) if (rank == 0 and world > 1) else None
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    kernel_ms = []
+
+    def step(timed):
+        counters.zero_()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        r.render_async(packed.data_ptr(), counters.data_ptr(), sptr, seed=a.seed)
+        ev1.record(stream)
+        if world > 1:
+            if rank == 0:
+                dist.gather(packed, gather_list=list(gathered.view(world, -1).unbind(0)), dst=0)
+                r.unpack_async(gathered.data_ptr(), frame.data_ptr(), world, sptr)
+            else:
+                dist.gather(packed, dst=0)
+        else:
+            r.unpack_async(packed.data_ptr(), frame.data_ptr(), 1, sptr)
+        if timed:
+            kernel_ms.append((ev0, ev1))
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tot = torch.zeros(16, dtype=torch.int64, device=dev)
+    for _ in range(a.steps):
+        step(True)
+        tot += counters
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kms = [e0.elapsed_time(e1) for e0, e1 in kernel_ms]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        km = torch.tensor([sum(kms) / len(kms)], dtype=torch.float64, device=dev)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        kernel_avg_ms = float(km.item())
+    else:
+        kernel_avg_ms = sum(kms) / len(kms)
+
+    from grayshift_amd._native import COUNTER_NAMES
+    c = {n: int(tot[i].item()) // a.steps for i, n in enumerate(COUNTER_NAMES)}
+    rays_per_frame = c["rays"]
+    value = rays_per_frame * a.steps / elapsed / 1e6
+    abytes = algorithmic_bytes(c) / max(1, world)  # per launch (per rank)
+    achieved = abytes / (kernel_avg_ms / 1e3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        cpu = cpu_baseline(sc, a)
+
+    traffic = None
+    if a.traffic and os.path.exists(a.traffic):
+        with open(a.traffic) as f:
+            tj = json.load(f)
+        if tj.get("config") == a.config and tj.get("hbm_bytes_per_launch"):
+            traffic = tj["hbm_bytes_per_launch"]
+
+    if rank == 0:
+        if a.dump:
+            import numpy as np
+            np.save(a.dump, frame.view(r.height, r.width, 3).cpu().numpy())
+        invalid = a.width is not None or a.spp is not None
+        out = {
+            "metric": "Msamples/sec (primary+secondary rays)",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (deterministic scene generator, seed 'grayshif'; decoded reference assets)",
+            "config": {
+                "workload": "%s: %s %dx%d, %d spp%s" % (a.config, sc.name, r.width, r.height,
+                                                      sc.settings.batch_size,
+                                                      " (OVERRIDDEN: not the metric)" if invalid else ""),
+                "tile": a.tile, "parallelism": "tiles%d" % world, "seed": a.seed,
+                "rays_per_frame": rays_per_frame, "paths_per_frame": c["paths"],
+                "node_visits_per_ray": round(c["node_visits"] / max(1, rays_per_frame), 3),
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel_ms": round(kernel_avg_ms, 3), "algorithmic_bytes_per_launch": int(abytes),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    r.close()
+
+
+def cpu_baseline(sc, a):
+    """The CPU oracle on every cpu_stride-th row and column of the same frame."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test-infrastructure checker, used here only as the CPU baseline
+    threads = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    W, H, s = sc.width, sc.height, a.cpu_stride
+    sub = np.array([j * W + i for j in range(0, H, s) for i in range(0, W, s)], dtype=np.int32)
+    t0 = time.perf_counter()
+    _, c = oracle.render(sc, seed=a.seed, threads=threads, subset=sub)
+    dt = time.perf_counter() - t0
+    return {"value": round(c["rays"] / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": "%d px (every %dth row/col of the frame) x %d spp = %d rays in %.1fs (incl. world/BVH build)"
+                      % (len(sub), s, sc.settings.batch_size, c["rays"], dt)}
+
+
+if __name__ == "__main__":
+    main()
