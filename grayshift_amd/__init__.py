@@ -3,13 +3,27 @@
 The product is ``libgrayshift.so``: a persistent-wavefront HIP megakernel for gfx950
 behind the C-ABI of include/grayshift_gpu.h, plus a C++ host mirror of the
 reference's Camera / Hittable / Material surface (include/grayshift_host.h).
-Importing this package loads that library and raises if it is missing; there is no
-CPU fallback.
-"""
-from . import _native  # noqa: F401  (loads libgrayshift.so or raises)
-from .render import HostScene, Renderer, camera, render, set_tuning, write_ppm  # noqa: F401
-from .scene import SceneBuilder, camera_spec, fixed_spp, sample_settings  # noqa: F401
-from . import scenes  # noqa: F401
 
-__all__ = ["HostScene", "Renderer", "camera", "render", "set_tuning", "write_ppm", "SceneBuilder",
-           "camera_spec", "fixed_spp", "sample_settings", "scenes"]
+The public names below load that library on first use and raise if it is missing
+(build it with ``python -m grayshift_amd.build``); there is no CPU fallback.
+``grayshift_amd.build`` itself imports without the library.
+"""
+import importlib
+
+_EXPORTS = {
+    "HostScene": "renderer", "Renderer": "renderer", "camera": "renderer", "render": "renderer",
+    "set_tuning": "renderer", "write_ppm": "renderer",
+    "SceneBuilder": "scene", "camera_spec": "scene", "fixed_spp": "scene", "sample_settings": "scene",
+}
+_SUBMODULES = {"scenes", "partition", "assets", "_native", "scene"}
+
+__all__ = sorted(_EXPORTS) + ["scenes"]
+
+
+def __getattr__(name):
+    if name in _EXPORTS:
+        mod = importlib.import_module("." + _EXPORTS[name], __name__)
+        return getattr(mod, name)
+    if name in _SUBMODULES:
+        return importlib.import_module("." + name, __name__)
+    raise AttributeError(name)

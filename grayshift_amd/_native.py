@@ -87,7 +87,12 @@ class gs_partition(C.Structure):
     _fields_ = [("rank", C.c_int32), ("world_size", C.c_int32), ("tile_w", C.c_int32), ("tile_h", C.c_int32)]
 
 
-class gs_flat_scene(C.Structure):  # only counts are read from Python
+class gs_background(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("width", C.c_uint32), ("height", C.c_uint32), ("pad", C.c_uint32),
+                ("color", D3), ("rot", C.c_double * 9)]
+
+
+class gs_flat_scene(C.Structure):
     _fields_ = [("root", C.c_uint32), ("max_bvh_depth", C.c_uint32),
                 ("nodes", C.c_void_p), ("n_nodes", C.c_uint32),
                 ("spheres", C.c_void_p), ("n_spheres", C.c_uint32),
@@ -100,7 +105,9 @@ class gs_flat_scene(C.Structure):  # only counts are read from Python
                 ("materials", C.c_void_p), ("n_materials", C.c_uint32),
                 ("textures", C.c_void_p), ("n_textures", C.c_uint32),
                 ("images", C.c_void_p), ("n_images", C.c_uint32),
-                ("texels8", C.c_void_p), ("n_texels8", C.c_uint64)]
+                ("texels8", C.c_void_p), ("n_texels8", C.c_uint64),
+                ("background", gs_background),
+                ("hdri_rgb", C.c_void_p), ("n_hdri_floats", C.c_uint64)]
 
 
 # Every symbol include/*.h declares, with its ctypes signature.
@@ -115,6 +122,8 @@ SIGNATURES = {
     "gs_partition_capacity": (C.c_int64, [C.POINTER(gs_camera), C.POINTER(gs_partition)]),
     "gs_render_tiles_async": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64,
                                           C.POINTER(gs_partition), _P, _P, _P]),
+    "gs_render_tiles_debug_async": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64,
+                                                C.POINTER(gs_partition), _P, _P, _P, _P]),
     "gs_unpack_tiles_async": (C.c_int32, [C.POINTER(gs_camera), C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P, _P,
                                           _P]),
     "gs_render": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64, _P,

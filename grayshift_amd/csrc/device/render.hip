@@ -85,6 +85,7 @@ struct KArgs {
     float* out;
     unsigned long long* counters;
     uint32_t* queue;
+    uint32_t* item_visits;  // diagnostic: node visits per packed pixel (nullable)
 };
 
 enum { S_NEED = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };
@@ -550,6 +551,7 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_render_kernel(KArgs A) {
                     o[1] = (float)(csg / scount);
                     o[2] = (float)(csb / scount);
                     atomicAdd(&s_cnt[C_PIX], 1ull);
+                    if (A.item_visits) A.item_visits[item] = c_nodes;
                     atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
                     atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
                     c_nodes = 0;
@@ -1045,6 +1047,12 @@ int64_t gs_partition_capacity(const gs_camera* cam, const gs_partition* p) {
 gs_status gs_render_tiles_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
                                 uint64_t seed, const gs_partition* part, float* d_out, gs_counters* d_counters,
                                 void* stream) {
+    return gs_render_tiles_debug_async(ds, cam, ss, seed, part, d_out, d_counters, nullptr, stream);
+}
+
+gs_status gs_render_tiles_debug_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
+                                      uint64_t seed, const gs_partition* part, float* d_out,
+                                      gs_counters* d_counters, uint32_t* d_item_visits, void* stream) {
     if (!ds || !cam || !ss || !part || !d_out) return fail(GS_ERR_ARG, "null argument");
     if (!part_ok(cam, part)) return fail(GS_ERR_ARG, "bad partition / image size");
     if (ss->batch_size == 0) return fail(GS_ERR_ARG, "batch_size 0 never terminates (camera.rs:137)");
@@ -1072,6 +1080,7 @@ gs_status gs_render_tiles_async(const gs_device_scene* ds, const gs_camera* cam,
     a.out = d_out;
     a.counters = (unsigned long long*)d_counters;
     a.queue = ds->queue;
+    a.item_visits = d_item_visits;
     HIPCHK(hipMemsetAsync(ds->queue, 0, 4, st));
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));

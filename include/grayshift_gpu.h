@@ -211,6 +211,13 @@ gs_status gs_render_tiles_async(const gs_device_scene* scene, const gs_camera* c
                                 const gs_partition* part, float* d_packed_rgb,
                                 gs_counters* d_counters, void* stream);
 
+/* Diagnostic variant: also writes, per packed pixel, the number of BVH node visits
+ * its samples made (d_item_visits: capacity u32, nullable). */
+gs_status gs_render_tiles_debug_async(const gs_device_scene* scene, const gs_camera* cam,
+                                      const gs_sample_settings* ss, uint64_t seed,
+                                      const gs_partition* part, float* d_packed_rgb,
+                                      gs_counters* d_counters, uint32_t* d_item_visits, void* stream);
+
 /* Scatter the packed buffers of all ranks (world_size * capacity * 3 f32, rank-major,
  * as a gather leaves them) into a W*H*3 frame.  Runs on the current device. */
 gs_status gs_unpack_tiles_async(const gs_camera* cam, int32_t world_size, int32_t tile_w,

@@ -60,6 +60,8 @@ def render(scene, seed=1, threads=0, subset=None):
     """Render `scene` (scenes.Scene) on the CPU.  Returns (rgb f32 [n,3] or [H,W,3], counters dict)."""
     from grayshift_amd import _native as N
     L = lib()
+    if not threads:  # the GPU box's CPU share is 16 cores; nproc reports the whole machine
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     cnt = N.gs_counters()
     if subset is not None:
         sub = np.ascontiguousarray(subset, dtype=np.int32)

@@ -1,0 +1,204 @@
+"""CPU tests of the product library: it loads, exports every declared symbol, its
+ctypes mirror matches the C layouts, and the C++ host mirror builds the same world,
+BVH and camera as the oracle.  No compute on a device."""
+import ctypes as C
+import hashlib
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import grayshift_amd as g
+from grayshift_amd import _native as N
+from grayshift_amd import partition, scenes
+from grayshift_amd.scene import SceneBuilder, fixed_spp
+import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = []
+    for h in ("grayshift_gpu.h", "grayshift_host.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s*(gs_[a-z0-9_]+)\s*\(", src, re.M):
+            names.append(m.group(1))
+    return names
+
+
+def test_every_declared_symbol_is_exported(built):
+    names = declared_functions()
+    assert len(names) >= 15
+    lib = C.CDLL(N.LIB_PATH)
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in N.SIGNATURES, "ctypes mirror lacks " + n
+
+
+def test_version_and_error_channel():
+    assert N.lib.gs_version() == 1
+    assert N.lib.gs_set_tuning(0, 0) == N.GS_ERR_ARG
+    assert b"tuning" in N.lib.gs_last_error()
+    assert N.lib.gs_set_tuning(32, 0) == N.GS_OK
+
+
+@pytest.mark.parametrize("name", ["gs_object", "gs_material_spec", "gs_texture_spec", "gs_image_spec",
+                                  "gs_background_spec", "gs_scene_spec", "gs_camera_spec", "gs_sample_settings",
+                                  "gs_counters", "gs_camera", "gs_partition", "gs_background", "gs_flat_scene"])
+def test_struct_layouts_match(name):
+    assert N.lib.gs_host_struct_size(name.encode()) == C.sizeof(getattr(N, name))
+
+
+def test_device_record_sizes():
+    # the per-unit record sizes DESIGN.md §5 prices
+    for name, size in [("gs_node", 64), ("gs_sphere", 40), ("gs_msphere", 64), ("gs_quad", 136),
+                       ("gs_triangle", 104), ("gs_instance", 32), ("gs_material", 40)]:
+        assert N.lib.gs_host_struct_size(name.encode()) == size, name
+
+
+ALL_SCENES = ["C1", "C3", "C4", "C5", "earth", "quads", "triangles", "checkered_spheres", "hdri", "cornell_box"]
+
+
+def _scene(name):
+    if name.startswith("C"):
+        return scenes.config(name, width=64, spp=4)
+    return scenes.SCENES[name](width=64)
+
+
+@pytest.mark.parametrize("name", ALL_SCENES)
+def test_bvh_topology_matches_oracle(name):
+    sc = _scene(name)
+    n = N.lib.gs_host_bvh_topology(sc.spec.ptr(), None, 0)
+    mine = np.zeros(n, np.int32)
+    N.lib.gs_host_bvh_topology(sc.spec.ptr(), mine.ctypes.data_as(C.POINTER(C.c_int32)), n)
+    assert np.array_equal(mine, oracle.bvh_topology(sc.spec))
+
+
+@pytest.mark.parametrize("name", ALL_SCENES + ["C2"])
+def test_camera_fields_bit_exact(name):
+    sc = scenes.config(name) if name.startswith("C") else scenes.SCENES[name]()
+    cam = g.camera(sc.camera)
+    mine = [cam.image_height] + [x for f in ("center", "starting_pixel_pos", "pixel_delta_u", "pixel_delta_v",
+                                            "defocus_disk_u", "defocus_disk_v") for x in getattr(cam, f)]
+    assert np.array_equal(np.array(mine, np.float64), oracle.camera_fields(sc.camera))
+
+
+def test_config_sizes():
+    for name, (w, h) in {"C1": (400, 225), "C2": (1920, 1080), "C3": (1024, 1024), "C4": (1920, 1080),
+                         "C5": (3840, 2160)}.items():
+        cam = g.camera(scenes.config(name).camera)
+        assert (cam.image_width, cam.image_height) == (w, h)
+
+
+def test_c4_world_is_the_10k_sphere_bvh():
+    hs = g.HostScene(scenes.config("C4").spec)
+    st = hs.stats()
+    assert st["spheres"] == 10002 and st["nodes"] == 11811 and st["max_bvh_depth"] == 14
+
+
+def test_scene_generator_is_deterministic():
+    a = scenes.config("C4").spec
+    b = scenes.config("C4").spec
+    ba = bytes(C.string_at(C.addressof(a.objects), a.spec.n_objects * C.sizeof(N.gs_object)))
+    bb = bytes(C.string_at(C.addressof(b.objects), b.spec.n_objects * C.sizeof(N.gs_object)))
+    assert ba == bb
+
+
+def test_assets_match_manifest():
+    from grayshift_amd import assets
+    man = json.load(open(os.path.join(ROOT, "grayshift_amd", "assets", "manifest.json")))
+    e = assets.earthmap_rgb8()
+    assert e.shape == (512, 1024, 3)
+    assert hashlib.sha256(e.tobytes()).hexdigest() == man["earthmap.jpg"]["decoded_sha256"]
+    h = assets.airport_hdr_f32()
+    assert h.shape == (512, 1024, 3) and h.dtype == np.float32 and float(h.max()) == 3808.0
+
+
+def test_rgbe_conversion():
+    from grayshift_amd.assets import rgbe_to_f32
+    px = np.array([[[128, 64, 0, 129], [255, 255, 255, 0], [1, 2, 3, 136]]], np.uint8)
+    out = rgbe_to_f32(px)
+    assert out[0, 0].tolist() == [1.0, 0.5, 0.0]     # m * 2^(129-136)
+    assert out[0, 1].tolist() == [0.0, 0.0, 0.0]     # e == 0 -> black
+    assert out[0, 2].tolist() == [1.0, 2.0, 3.0]
+
+
+@pytest.mark.parametrize("w,h,world,tile", [(1920, 1080, 1, 64), (1920, 1080, 8, 64), (400, 225, 3, 64),
+                                            (37, 23, 2, 16), (1, 1, 4, 8)])
+def test_partition_covers_every_pixel_once(w, h, world, tile):
+    seen = np.zeros(w * h, np.int32)
+    cam = N.gs_camera(image_width=w, image_height=h)
+    for r in range(world):
+        cap = N.lib.gs_partition_capacity(C.byref(cam), C.byref(N.gs_partition(r, world, tile, tile)))
+        assert cap == partition.capacity(w, h, r, world, tile, tile)
+        ids = partition.packed_pixel_ids(w, h, r, world, tile, tile)
+        np.add.at(seen, ids[ids >= 0], 1)
+    assert (seen == 1).all()
+
+
+def test_color_byte_matches_oracle():
+    for c in [0.0, 1e-9, 0.0625, 0.25, 0.5, 0.998, 0.999, 1.0, 7.0, -3.0, float("nan"), float("inf")]:
+        assert N.lib.gs_host_color_byte(c) == oracle.color_byte(c)
+
+
+def test_write_ppm(tmp_path):
+    rgb = np.array([[[0.0, 0.25, 1.0], [4.0, -1.0, 0.0625]]], np.float32)
+    p = str(tmp_path / "x.ppm")
+    g.write_ppm(p, rgb)
+    assert open(p).read() == "P3\n2 1\n255\n0 128 255\n255 0 64\n"
+
+
+# ---------------------------------------------------------------- errors
+def _flat_copy(name="C3"):
+    hs = g.HostScene(_scene(name).spec)
+    f = N.gs_flat_scene.from_buffer_copy(hs.flat)
+    return hs, f
+
+
+def test_malformed_scene_is_rejected_before_the_device():
+    hs, f = _flat_copy()
+    f.root = (1 << 28) | 9999  # node index out of range
+    out = C.c_void_p()
+    assert N.lib.gs_device_scene_create(C.byref(f), C.byref(out)) == N.GS_ERR_ARG
+    assert b"node index" in N.lib.gs_last_error()
+    hs, f = _flat_copy()
+    f.n_materials = 0
+    assert N.lib.gs_device_scene_create(C.byref(f), C.byref(out)) == N.GS_ERR_ARG
+
+
+def test_volume_material_is_unsupported():
+    b = SceneBuilder()
+    m = b._mat(N.GS_MAT_ISOTROPIC, b.solid((1, 1, 1)))
+    b.add(b.sphere((0, 0, 0), 1, m))
+    h = C.c_void_p()
+    assert N.lib.gs_host_scene_from_spec(b.build().ptr(), C.byref(h)) == N.GS_ERR_UNSUPPORTED
+
+
+def test_bvh_under_instance_is_unsupported():
+    b = SceneBuilder()
+    m = b.lambertian((1, 1, 1))
+    inner = b.bvh([b.sphere((0, 0, 0), 1, m), b.sphere((3, 0, 0), 1, m), b.sphere((6, 0, 0), 1, m)])
+    b.add(b.translate(inner, (1, 0, 0)))
+    h = C.c_void_p()
+    assert N.lib.gs_host_scene_from_spec(b.build().ptr(), C.byref(h)) == N.GS_ERR_UNSUPPORTED
+
+
+def test_empty_world_is_an_error():
+    h = C.c_void_p()
+    assert N.lib.gs_host_scene_from_spec(SceneBuilder().build().ptr(), C.byref(h)) == N.GS_ERR_ARG
+
+
+def test_no_cpu_fallback_without_device():
+    # Without a GPU the product must fail loudly, never compute on the CPU.
+    import subprocess
+    import sys
+    code = ("import grayshift_amd as g; from grayshift_amd import scenes\n"
+            "try:\n g.render(scenes.config('C1', width=8, spp=1))\n"
+            "except g._native.GrayshiftError as e: print('ERR', e.code)\n"
+            "else: print('RENDERED')\n")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert "ERR" in r.stdout, r.stdout + r.stderr
