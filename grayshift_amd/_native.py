@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgrayshift.so")
+LIB_PATH = os.environ.get("GS_LIB") or os.path.join(HERE, "libgrayshift.so")  # GS_LIB: A/B variant builds
 
 # ------------------------------------------------------------------ enums
 GS_OBJ_SPHERE, GS_OBJ_MOVING_SPHERE, GS_OBJ_QUAD, GS_OBJ_TRIANGLE = 1, 2, 3, 4

@@ -48,12 +48,15 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build_product(force=False, verbose=False, extra=()):
-    if not force and not _stale(LIB, DEPS):
-        return LIB
+def build_product(force=False, verbose=False, extra=(), out=None):
+    """Build libgrayshift.so (or a variant at `out` with extra compiler flags)."""
+    lib = out or LIB
+    if not force and not _stale(lib, DEPS):
+        return lib
     objs = []
+    tag = "" if out is None else "_" + os.path.basename(out).replace(".so", "")
     for src in SOURCES:
-        obj = os.path.join(HERE, "csrc", "_obj", os.path.basename(src) + ".o")
+        obj = os.path.join(HERE, "csrc", "_obj" + tag, os.path.basename(src) + ".o")
         os.makedirs(os.path.dirname(obj), exist_ok=True)
         cmd = [HIPCC] + COMMON + list(extra)
         if src.endswith(".hip"):
@@ -63,13 +66,13 @@ def build_product(force=False, verbose=False, extra=()):
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", tmp] + objs + ["-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 def build_oracle(force=False, verbose=False):
@@ -85,11 +88,19 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--no-oracle", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--variant", action="append", metavar="NAME:FLAGS", default=[],
+                    help="also build variants/NAME.so with extra FLAGS (A/B), e.g. --variant 'v4:-DGS_MIN_WAVES=4'")
     ap.add_argument("--resource-usage", action="store_true",
                     help="print per-kernel VGPR/SGPR/LDS/occupancy (hipcc remarks)")
     a = ap.parse_args(argv)
     extra = ["-Rpass-analysis=kernel-resource-usage"] if a.resource_usage else []
     build_product(force=a.force or a.resource_usage, verbose=a.verbose, extra=extra)
+    for spec in a.variant:
+        name, _, flags = spec.partition(":")
+        path = os.path.join(HERE, "variants", name + ".so")
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        build_product(force=True, verbose=a.verbose, extra=extra + flags.split(), out=path)
+        print("variant", path, flags)
     if not a.no_oracle:
         build_oracle(force=a.force, verbose=a.verbose)
     print("built", LIB, "" if a.no_oracle else ORACLE_LIB)

@@ -36,7 +36,15 @@
 using namespace gsd;
 
 #define GS_BLOCK 256
-#define GS_STACK 32
+#define GS_STACK 32  // max BVH depth the device accepts
+// Measured on MI355X (C4): everything inlined with a 4-waves/SIMD register cap (128
+// VGPRs; spills only in shading) beats out-of-line shading calls and 3 or 5 waves.
+#ifndef GS_NOINLINE
+#define GS_NOINLINE __forceinline__
+#endif
+#ifndef GS_MIN_WAVES
+#define GS_MIN_WAVES 4
+#endif
 #define GS_MAX_CHAIN 4
 
 // ---------------------------------------------------------------- device layout
@@ -201,17 +209,23 @@ __device__ __forceinline__ void inst_backward(const gs_instance& in, d3& p, d3& 
     }
 }
 
-// Test one primitive ref against `ray` (already in the primitive's space).
-// Accepts -> closest/hit_ref updated ("last accepted wins", as BVH.rs:73-80 and
-// hittable.rs:75-83 compose).
+// Outcome of testing one non-node child against the ray.
+struct LeafHit {
+    bool hit;
+    double t;
+    uint32_t ref, inst;
+};
+
+// One primitive ref against `ray` (already in the primitive's space); accepts into
+// `res` ("last accepted wins", as BVH.rs:73-80 and hittable.rs:75-83 compose).
 __device__ __forceinline__ void prim_test(const DevScene& sc, uint32_t ref, const Ray& ray, double tmin,
-                                          double& closest, uint32_t& hit_ref, uint32_t& hit_inst, uint32_t inst_ref,
-                                          unsigned long long* cnt, uint32_t& c_sph) {
+                                          double closest, uint32_t inst_ref, LeafHit& res,
+                                          unsigned long long* cnt) {
     const uint32_t kind = ref >> GS_REF_SHIFT, idx = ref & GS_REF_MASK;
     double t;
     bool ok = false;
     if (kind == GS_REF_SPHERE) {
-        c_sph++;
+        atomicAdd(&cnt[C_SPH], 1ull);
         DSphere s = sc.spheres[idx];
         ok = sphere_accept(mk(s.cx, s.cy, s.cz), s.r, ray, len2(ray.d), tmin, closest, t);
     } else if (kind == GS_REF_MSPHERE) {
@@ -228,19 +242,25 @@ __device__ __forceinline__ void prim_test(const DevScene& sc, uint32_t ref, cons
         ok = tri_hit(sc.tris[idx], ray, t, u, v);
     }
     if (ok) {
-        closest = t;
-        hit_ref = ref;
-        hit_inst = inst_ref;
+        res.hit = true;
+        res.t = t;
+        res.ref = ref;
+        res.inst = inst_ref;
     }
 }
 
-// A non-node child: primitive, list, or instance chain (→ list or primitive).
-__device__ __noinline__ void leaf_test(const DevScene& sc, uint32_t ref, const Ray& ray, double tmin, double& closest,
-                                       uint32_t& hit_ref, uint32_t& hit_inst, unsigned long long* cnt,
-                                       uint32_t& c_sph) {
+// The rarer non-node children (everything but a stationary sphere reached directly
+// from a BVH node): moving sphere, quad, triangle, HittableList, Translate/RotateY
+// chain.  Kept out of line so it does not inflate the traversal loop's registers.
+__device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, uint32_t ref, Ray r, double tmin, double closest,
+                                           unsigned long long* cnt) {
+    LeafHit res;
+    res.hit = false;
+    res.t = closest;
+    res.ref = GS_REF_NONE;
+    res.inst = GS_REF_NONE;
     uint32_t kind = ref >> GS_REF_SHIFT;
     uint32_t inst_ref = GS_REF_NONE;
-    Ray r = ray;
     uint32_t cur = ref;
     if (kind == GS_REF_INSTANCE) {
         inst_ref = ref;
@@ -258,17 +278,18 @@ __device__ __noinline__ void leaf_test(const DevScene& sc, uint32_t ref, const R
         const gs_list l = sc.lists[cur & GS_REF_MASK];
 #pragma unroll 1
         for (uint32_t k = 0; k < l.count; k++)
-            prim_test(sc, sc.list_refs[l.first + k], r, tmin, closest, hit_ref, hit_inst, inst_ref, cnt, c_sph);
+            prim_test(sc, sc.list_refs[l.first + k], r, tmin, res.t, inst_ref, res, cnt);
     } else {
-        prim_test(sc, cur, r, tmin, closest, hit_ref, hit_inst, inst_ref, cnt, c_sph);
+        prim_test(sc, cur, r, tmin, closest, inst_ref, res, cnt);
     }
+    return res;
 }
 
 struct HitRec {
     d3 p, n;
-    bool front;
     double u, v;
     uint32_t mat;
+    bool front;
 };
 
 __device__ __forceinline__ void sphere_uv(d3 p, double& u, double& v) {  // sphere.rs:55-60
@@ -281,9 +302,9 @@ __device__ __forceinline__ void sphere_uv(d3 p, double& u, double& v) {  // sphe
 
 // Recompute the HitRecord of the accepted primitive at t (the values the reference
 // built when it accepted it), then apply the instance back-transforms innermost-first.
-__device__ __noinline__ void reconstruct(const DevScene& sc, const Ray& ray, double t, uint32_t hit_ref,
-                                         uint32_t hit_inst, HitRec& h) {
-    Ray r = ray;
+__device__ GS_NOINLINE HitRec reconstruct(const DevScene& sc, Ray r, double t, uint32_t hit_ref,
+                                           uint32_t hit_inst) {
+    HitRec h;
     uint32_t ch0 = 0, ch1 = 0, ch2 = 0, ch3 = 0;
     int nch = 0;
     if (hit_inst != GS_REF_NONE) {
@@ -347,10 +368,11 @@ __device__ __noinline__ void reconstruct(const DevScene& sc, const Ray& ray, dou
     h.n = n;
     h.u = u;
     h.v = v;
+    return h;
 }
 
 // Texture::value_at (texture.rs:27-95); checkered nesting resolved iteratively.
-__device__ __noinline__ d3 texture_value(const DevScene& sc, uint32_t tex, double u, double v, d3 p,
+__device__ GS_NOINLINE d3 texture_value(const DevScene& sc, uint32_t tex, double u, double v, d3 p,
                                          unsigned long long* cnt) {
 #pragma unroll 1
     for (int depth = 0; depth < 16; depth++) {
@@ -384,7 +406,7 @@ __device__ __noinline__ d3 texture_value(const DevScene& sc, uint32_t tex, doubl
 }
 
 // Camera::sample_background / HDRI::sample (camera.rs:228-233, 257-270).
-__device__ __noinline__ d3 background(const DevScene& sc, d3 dir, unsigned long long* cnt) {
+__device__ GS_NOINLINE d3 background(const DevScene& sc, d3 dir, unsigned long long* cnt) {
     const gs_background& bg = sc.bg;
     if (bg.kind == GS_BG_SOLID) return ld3(bg.color);
     const double PI = 3.14159265358979323846;
@@ -416,15 +438,24 @@ __device__ __forceinline__ d3 random_unit_vector(uint64_t& rng) {  // util.rs:18
     return unit(v);
 }
 
-// Material::scatter (material.rs).  Returns false when the path ends (absorbed /
-// emitter); `att` and the new ray are set when it continues.  `emit` gets the
-// emitted colour (DiffuseLight only; every other material emits zero).
-__device__ __noinline__ bool scatter(const DevScene& sc, const HitRec& h, Ray& ray, uint64_t& rng, d3& att, d3& emit,
-                                     bool& emits, unsigned long long* cnt) {
+// Material::emitted + Material::scatter (material.rs).  kind: 0 = path ends with
+// `col` (emitted colour; 0 for an absorbed ray), 1 = continues along `dir` with
+// attenuation `col`.
+struct Scatter {
+    d3 col, dir;
+    uint64_t rng;
+    uint32_t cont;
+};
+
+__device__ GS_NOINLINE Scatter scatter(const DevScene& sc, HitRec h, d3 in_dir, uint64_t rng,
+                                        unsigned long long* cnt) {
     const DMaterial& m = sc.mats[h.mat];
-    emits = false;
+    Scatter s;
+    s.cont = 0;
+    s.col = mk(0.0, 0.0, 0.0);
+    s.dir = mk(0.0, 0.0, 0.0);
     if (m.kind == GS_MAT_LAMBERTIAN) {  // :45-68
-        att = texture_value(sc, m.texture, h.u, h.v, h.p, cnt);
+        s.col = texture_value(sc, m.texture, h.u, h.v, h.p, cnt);
         // OrthonormalBasis::new (ONB.rs:10-23)
         d3 w = unit(h.n);
         d3 a = fabs(w.x) > 0.9 ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);
@@ -440,25 +471,19 @@ __device__ __noinline__ bool scatter(const DevScene& sc, const HitRec& h, Ray& r
         sincos(phi, &sp, &cp);
         double q = sqrt(r2s);
         d3 cd = mk(cp * q, sp * q, sqrt(1.0 - r2));
-        d3 dir = unit(add(add(muls(uu, cd.x), muls(vv, cd.y)), muls(w, cd.z)));
-        ray.o = h.p;
-        ray.d = dir;
-        return true;
-    }
-    if (m.kind == GS_MAT_METAL) {  // :87-102
-        d3 reflected = reflect(ray.d, h.n);
+        s.dir = unit(add(add(muls(uu, cd.x), muls(vv, cd.y)), muls(w, cd.z)));
+        s.cont = 1;
+    } else if (m.kind == GS_MAT_METAL) {  // :87-102
+        d3 reflected = reflect(in_dir, h.n);
         reflected = add(unit(reflected), muls(random_unit_vector(rng), m.param));
         if (dot(reflected, h.n) > 0.0) {
-            att = ld3(m.albedo);
-            ray.o = h.p;
-            ray.d = reflected;
-            return true;
+            s.col = ld3(m.albedo);
+            s.dir = reflected;
+            s.cont = 1;
         }
-        return false;
-    }
-    if (m.kind == GS_MAT_DIELECTRIC) {  // :123-148
+    } else if (m.kind == GS_MAT_DIELECTRIC) {  // :123-148
         double ri = h.front ? 1.0 / m.param : m.param;
-        d3 ud = unit(ray.d);
+        d3 ud = unit(in_dir);
         double cos_theta = fmin(dot(neg(ud), h.n), 1.0);
         double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
         bool cannot_refract = ri * sin_theta > 1.0;
@@ -469,25 +494,33 @@ __device__ __noinline__ bool scatter(const DevScene& sc, const HitRec& h, Ray& r
         double x4 = x2 * x2;
         double refl = r0 + (1.0 - r0) * (x * x4);  // powi(x, 5) as LLVM expands it
         bool fresnel = refl > wy_f64(rng);
-        d3 dir = (cannot_refract || fresnel) ? reflect(ud, h.n) : refract(ud, h.n, ri);
-        att = mk(1.0, 1.0, 1.0);
-        ray.o = h.p;
-        ray.d = dir;
-        return true;
+        s.dir = (cannot_refract || fresnel) ? reflect(ud, h.n) : refract(ud, h.n, ri);
+        s.col = mk(1.0, 1.0, 1.0);
+        s.cont = 1;
+    } else if (m.kind == GS_MAT_DIFFUSE_LIGHT) {  // :165-169 (emits, never scatters)
+        s.col = texture_value(sc, m.texture, h.u, h.v, h.p, cnt);
     }
-    if (m.kind == GS_MAT_DIFFUSE_LIGHT) {  // :165-169 (no scatter)
-        emit = texture_value(sc, m.texture, h.u, h.v, h.p, cnt);
-        emits = true;
-        return false;
-    }
-    return false;
+    s.rng = rng;
+    return s;
 }
 
 __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull << lane) - 1ull; }
 
-__global__ __launch_bounds__(GS_BLOCK) void gs_render_kernel(KArgs A) {
-    __shared__ uint32_t s_stack[GS_STACK * GS_BLOCK];
+// Per-lane pixel state lives in LDS ([field][lane], conflict-free), touched once per
+// path; the traversal stack follows it: [depth][lane] u32 refs.
+enum { L_CSR = 0, L_CSG, L_CSB, L_LSUM, L_LSQ, L_SCOUNT, L_ND };
+enum { L_ITEM = 0, L_PIX, L_BLEFT, L_NI };
+
+__host__ __device__ inline size_t lds_bytes(uint32_t stack_depth) {
+    return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4 + stack_depth * 4);
+}
+
+__global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs A) {
+    extern __shared__ __align__(16) uint8_t smem[];
     __shared__ unsigned long long s_cnt[C_N];
+    double* s_d = (double*)smem;                                  // [L_ND][GS_BLOCK]
+    uint32_t* s_i = (uint32_t*)(smem + L_ND * 8 * GS_BLOCK);      // [L_NI][GS_BLOCK]
+    uint32_t* s_stack = s_i + L_NI * GS_BLOCK;                    // [depth][GS_BLOCK]
     if (threadIdx.x < C_N) s_cnt[threadIdx.x] = 0;
     __syncthreads();
 
@@ -500,18 +533,15 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_render_kernel(KArgs A) {
     const bool blocked8 = (A.tile_w % 8 == 0) && (A.tile_h % 8 == 0);
     const double confidence_sq = A.ss.confidence * A.ss.confidence;
     const double tolerance_sq = A.ss.tolerance * A.ss.tolerance;
+#define LD(k) s_d[(k) * GS_BLOCK + tid]
+#define LI(k) s_i[(k) * GS_BLOCK + tid]
 
     uint32_t st = S_NEED;
     bool qdone = false;
-
-    // pixel state
-    uint32_t item = 0, pix = 0, sample = 0, batch_left = 0;
-    int32_t pi = 0, pj = 0;
-    double scount = 0.0, csr = 0.0, csg = 0.0, csb = 0.0, lsum = 0.0, lsq = 0.0;
-    // path state
+    // path state (registers)
+    uint32_t sample = 0, depth = 0;
     uint64_t rng = 0;
-    double Lr = 0, Lg = 0, Lb = 0, Tr = 1, Tg = 1, Tb = 1;
-    uint32_t depth = 0;
+    double Tr = 1, Tg = 1, Tb = 1;
     Ray ray;
     ray.o = mk(0, 0, 0);
     ray.d = mk(0, 0, 0);
@@ -533,23 +563,37 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_render_kernel(KArgs A) {
         atomicAdd(&s_cnt[C_RAYS], 1ull);
     };
 
-    // Start samples until one needs tracing or the pixel is finished.
-    // Returns with st = S_TRACE (ray ready) or S_NEED (pixel written).
-    auto next_sample = [&]() {
+    // camera.rs:142-146 for one finished sample of colour L
+    auto add_sample = [&](double Lr, double Lg, double Lb) {
+        LD(L_CSR) += Lr;
+        LD(L_CSG) += Lg;
+        LD(L_CSB) += Lb;
+        double lum = 0.299 * Lr + 0.587 * Lg + 0.144 * Lb;
+        LD(L_LSUM) += lum;
+        LD(L_LSQ) += lum * lum;
+        sample++;
+        LI(L_BLEFT) -= 1u;
+    };
+
+    // Start samples until one needs tracing or the pixel is finished:
+    // leaves st = S_TRACE (ray ready) or S_NEED (pixel written).
+    auto advance = [&]() {
 #pragma unroll 1
         for (;;) {
-            if (batch_left == 0) {
+            if (LI(L_BLEFT) == 0) {
                 // end of a batch (camera.rs:149-164)
+                const double scount = LD(L_SCOUNT), lsum = LD(L_LSUM), lsq = LD(L_LSQ);
                 double mean = lsum / scount;
                 double variance_sq = 1.0 / (scount - 1.0) * (lsq - lsum * lsum / scount);
                 double convergence_sq = confidence_sq * variance_sq / scount;
                 bool stop = convergence_sq < (mean * mean * tolerance_sq);
                 if (!stop) stop = (uint32_t)sat_u64(scount, 4294967295.0, 4294967295ull) > A.ss.max_samples;
                 if (stop) {
+                    const uint32_t item = LI(L_ITEM);
                     float* o = A.out + (size_t)item * 3;
-                    o[0] = (float)(csr / scount);
-                    o[1] = (float)(csg / scount);
-                    o[2] = (float)(csb / scount);
+                    o[0] = (float)(LD(L_CSR) / scount);
+                    o[1] = (float)(LD(L_CSG) / scount);
+                    o[2] = (float)(LD(L_CSB) / scount);
                     atomicAdd(&s_cnt[C_PIX], 1ull);
                     if (A.item_visits) A.item_visits[item] = c_nodes;
                     atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
@@ -559,10 +603,12 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_render_kernel(KArgs A) {
                     st = S_NEED;
                     return;
                 }
-                scount += (double)A.ss.batch_size;
-                batch_left = A.ss.batch_size;
+                LD(L_SCOUNT) = scount + (double)A.ss.batch_size;
+                LI(L_BLEFT) = A.ss.batch_size;
             }
             // Camera::get_ray (camera.rs:204-221) on the seeded stream of this sample
+            const uint32_t pix = LI(L_PIX);
+            const uint32_t pi = pix % (uint32_t)cam.image_width, pj = pix / (uint32_t)cam.image_width;
             rng = stream_seed(A.seed, pix, sample);
             atomicAdd(&s_cnt[C_PATHS], 1ull);
             double offx = wy_f64(rng) - 0.5;
@@ -586,7 +632,6 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_render_kernel(KArgs A) {
             ray.o = org;
             ray.d = sub(ps, org);
             ray.time = wy_f64(rng);
-            Lr = Lg = Lb = 0.0;
             Tr = Tg = Tb = 1.0;
             depth = cam.max_depth;
             if (depth > 0) {
@@ -594,26 +639,8 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_render_kernel(KArgs A) {
                 st = S_TRACE;
                 return;
             }
-            // ray_color(ray, 0) = 0: the sample contributes black (camera.rs:175)
-            sample++;
-            batch_left--;
-            // pixel_color += 0; lum = 0
-            lsum += 0.0;
-            lsq += 0.0;
+            add_sample(0.0, 0.0, 0.0);  // ray_color(ray, 0) = 0 (camera.rs:175)
         }
-    };
-
-    auto end_path = [&]() {
-        // camera.rs:142-146
-        csr += Lr;
-        csg += Lg;
-        csb += Lb;
-        double lum = 0.299 * Lr + 0.587 * Lg + 0.144 * Lb;
-        lsum += lum;
-        lsq += lum * lum;
-        sample++;
-        batch_left--;
-        next_sample();
     };
 
 #pragma unroll 1
@@ -644,26 +671,28 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_render_kernel(KArgs A) {
                         x = w % (uint32_t)A.tile_w;
                         y = w / (uint32_t)A.tile_w;
                     }
-                    item = slot * tile_px + y * (uint32_t)A.tile_w + x;
+                    const uint32_t item = slot * tile_px + y * (uint32_t)A.tile_w + x;
                     const uint32_t tile = (uint32_t)A.rank + slot * (uint32_t)A.world_size;
-                    pi = (int32_t)((tile % (uint32_t)A.tiles_x) * (uint32_t)A.tile_w + x);
-                    pj = (int32_t)((tile / (uint32_t)A.tiles_x) * (uint32_t)A.tile_h + y);
-                    if (pi >= cam.image_width || pj >= cam.image_height) {
+                    const uint32_t pi = (tile % (uint32_t)A.tiles_x) * (uint32_t)A.tile_w + x;
+                    const uint32_t pj = (tile / (uint32_t)A.tiles_x) * (uint32_t)A.tile_h + y;
+                    if (pi >= (uint32_t)cam.image_width || pj >= (uint32_t)cam.image_height) {
                         float* o = A.out + (size_t)item * 3;  // padding pixel
                         o[0] = 0.0f;
                         o[1] = 0.0f;
                         o[2] = 0.0f;
                     } else {
-                        pix = (uint32_t)pj * (uint32_t)cam.image_width + (uint32_t)pi;
-                        sample = 0;
-                        batch_left = 0;
-                        scount = 0.0;
-                        csr = csg = csb = 0.0;
-                        lsum = lsq = 0.0;
+                        LI(L_ITEM) = item;
+                        LI(L_PIX) = pj * (uint32_t)cam.image_width + pi;
+                        LD(L_CSR) = 0.0;
+                        LD(L_CSG) = 0.0;
+                        LD(L_CSB) = 0.0;
+                        LD(L_LSUM) = 0.0;
+                        LD(L_LSQ) = 0.0;
                         // first batch starts (camera.rs:137)
-                        scount += (double)A.ss.batch_size;
-                        batch_left = A.ss.batch_size;
-                        next_sample();
+                        LD(L_SCOUNT) = 0.0 + (double)A.ss.batch_size;
+                        LI(L_BLEFT) = A.ss.batch_size;
+                        sample = 0;
+                        advance();
                     }
                 }
             }
@@ -692,8 +721,23 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_render_kernel(KArgs A) {
                     } else {
                         cur = GS_REF_NONE;
                     }
+                } else if (kind == GS_REF_SPHERE) {
+                    c_sph++;
+                    const DSphere s = sc.spheres[cur & GS_REF_MASK];
+                    double t;
+                    if (sphere_accept(mk(s.cx, s.cy, s.cz), s.r, ray, len2(ray.d), tmin, closest, t)) {
+                        closest = t;
+                        hit_ref = cur;
+                        hit_inst = GS_REF_NONE;
+                    }
+                    cur = GS_REF_NONE;
                 } else {
-                    leaf_test(sc, cur, ray, tmin, closest, hit_ref, hit_inst, s_cnt, c_sph);
+                    const LeafHit lh = leaf_other(sc, cur, ray, tmin, closest, s_cnt);
+                    if (lh.hit) {
+                        closest = lh.t;
+                        hit_ref = lh.ref;
+                        hit_inst = lh.inst;
+                    }
                     cur = GS_REF_NONE;
                 }
                 if (cur == GS_REF_NONE) {
@@ -709,42 +753,46 @@ __global__ __launch_bounds__(GS_BLOCK) void gs_render_kernel(KArgs A) {
 
         // ---------------------------------------------------------- shade
         if (st == S_SHADE) {
+            bool ends = true;
+            double Lr = 0.0, Lg = 0.0, Lb = 0.0;
             if (hit_ref == GS_REF_NONE) {
-                // miss: sample_background (camera.rs:201)
-                d3 bg = background(sc, ray.d, s_cnt);
-                Lr = Lr + Tr * bg.x;
-                Lg = Lg + Tg * bg.y;
-                Lb = Lb + Tb * bg.z;
-                end_path();
+                // miss: sample_background (camera.rs:201); the path's only radiance
+                const d3 bg = background(sc, ray.d, s_cnt);
+                Lr = Tr * bg.x;
+                Lg = Tg * bg.y;
+                Lb = Tb * bg.z;
             } else {
                 atomicAdd(&s_cnt[C_HITS], 1ull);
-                HitRec h;
-                reconstruct(sc, ray, closest, hit_ref, hit_inst, h);
-                d3 att = mk(0, 0, 0), emit = mk(0, 0, 0);
-                bool emits = false;
-                bool cont = scatter(sc, h, ray, rng, att, emit, emits, s_cnt);
-                if (emits) {
-                    Lr = Lr + Tr * emit.x;
-                    Lg = Lg + Tg * emit.y;
-                    Lb = Lb + Tb * emit.z;
-                }
-                if (cont) {
-                    Tr = Tr * att.x;
-                    Tg = Tg * att.y;
-                    Tb = Tb * att.z;
+                const HitRec h = reconstruct(sc, ray, closest, hit_ref, hit_inst);
+                const Scatter s = scatter(sc, h, ray.d, rng, s_cnt);
+                rng = s.rng;
+                if (s.cont) {
+                    Tr = Tr * s.col.x;
+                    Tg = Tg * s.col.y;
+                    Tb = Tb * s.col.z;
                     depth--;
                     if (depth > 0) {
+                        ray.o = h.p;
+                        ray.d = s.dir;
                         begin_ray();
                         st = S_TRACE;
-                    } else {
-                        end_path();  // ray_color(.., 0) = 0 (camera.rs:175)
-                    }
+                        ends = false;
+                    }  // else ray_color(.., 0) = 0 (camera.rs:175): black
                 } else {
-                    end_path();
+                    // emitter (DiffuseLight never scatters) or absorbed (col = 0)
+                    Lr = Tr * s.col.x;
+                    Lg = Tg * s.col.y;
+                    Lb = Tb * s.col.z;
                 }
+            }
+            if (ends) {
+                add_sample(Lr, Lg, Lb);
+                advance();
             }
         }
     }
+#undef LD
+#undef LI
 
     // flush counters: LDS -> global, one atomic per counter per block
     atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
@@ -797,6 +845,7 @@ struct gs_device_scene {
     uint32_t* queue = nullptr;
     DevScene dev{};
     uint32_t n_nodes = 0;
+    uint32_t stack_depth = 1;  // LDS stack entries per lane (= BVH depth)
 };
 
 namespace {
@@ -813,7 +862,7 @@ struct Layout {
 
 // Host-side validation of everything the kernel indexes, so a malformed scene is an
 // error code, never a GPU fault.
-gs_status validate(const gs_flat_scene& s) {
+gs_status validate(const gs_flat_scene& s, uint32_t* depth_out) {
     auto bad = [](const std::string& m) { return fail(GS_ERR_ARG, "invalid flat scene: " + m); };
     auto unsup = [](const std::string& m) { return fail(GS_ERR_UNSUPPORTED, m); };
     if (!s.nodes && s.n_nodes) return bad("nodes");
@@ -876,6 +925,7 @@ gs_status validate(const gs_flat_scene& s) {
         }
     }
     if (maxd > GS_STACK) return unsup("BVH deeper than the device stack (" + std::to_string(GS_STACK) + ")");
+    *depth_out = maxd;
     auto mat_ok = [&](uint32_t m) { return m < s.n_materials; };
     for (uint32_t i = 0; i < s.n_spheres; i++) if (!mat_ok(s.spheres[i].material)) return bad("sphere material");
     for (uint32_t i = 0; i < s.n_mspheres; i++) if (!mat_ok(s.mspheres[i].material)) return bad("msphere material");
@@ -941,7 +991,8 @@ gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu) {
 gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) {
     if (!s || !out) return fail(GS_ERR_ARG, "null argument");
     *out = nullptr;
-    gs_status v = validate(*s);
+    uint32_t depth = 1;
+    gs_status v = validate(*s, &depth);
     if (v != GS_OK) return v;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GS_ERR_NO_DEVICE, "no HIP device visible");
@@ -1019,6 +1070,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     d.root = s->root;
     ds->queue = (uint32_t*)(b + o_queue);
     ds->n_nodes = s->n_nodes;
+    ds->stack_depth = depth < 1 ? 1 : depth;
     *out = ds;
     return GS_OK;
 }
@@ -1084,10 +1136,11 @@ gs_status gs_render_tiles_debug_async(const gs_device_scene* ds, const gs_camera
     HIPCHK(hipMemsetAsync(ds->queue, 0, 4, st));
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const size_t lds = lds_bytes(ds->stack_depth);
     int per_cu = g_blocks_per_cu;
     if (per_cu <= 0) {
         int occ = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gs_render_kernel, GS_BLOCK, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gs_render_kernel, GS_BLOCK, lds));
         per_cu = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
     }
     int64_t blocks = (int64_t)cus * per_cu;
@@ -1095,7 +1148,7 @@ gs_status gs_render_tiles_debug_async(const gs_device_scene* ds, const gs_camera
     int64_t max_blocks = (cap + GS_BLOCK - 1) / GS_BLOCK;
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(gs_render_kernel, dim3((unsigned)blocks), dim3(GS_BLOCK), 0, st, a);
+    hipLaunchKernelGGL(gs_render_kernel, dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
     return GS_OK;
 }
