@@ -103,6 +103,23 @@ struct Ray {
     double time;
 };
 
+__device__ __forceinline__ DNode load_node(const DNode* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+    DNode n;
+    n.mnx = __hiloint2double((int)a.y, (int)a.x);
+    n.mny = __hiloint2double((int)a.w, (int)a.z);
+    n.mnz = __hiloint2double((int)b.y, (int)b.x);
+    n.mxx = __hiloint2double((int)b.w, (int)b.z);
+    n.mxy = __hiloint2double((int)c.y, (int)c.x);
+    n.mxz = __hiloint2double((int)c.w, (int)c.z);
+    n.left = d.x;
+    n.right = d.y;
+    n.pad0 = d.z;
+    n.pad1 = d.w;
+    return n;
+}
+
 // AABB::hit (AABB.rs:58-113) with the reference's 1.0/d hoisted per ray (same value).
 // The early-outs of the reference do not change the boolean: once max <= min the
 // later slabs only raise min / lower max, and NaN slabs never assign.
@@ -710,17 +727,15 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             if (st == S_TRACE) {
                 const uint32_t kind = cur >> GS_REF_SHIFT;
                 if (kind == GS_REF_NODE) {
-                    const DNode nd = sc.nodes[cur & GS_REF_MASK];
+                    // All 64 B in one go (4 x dwordx4) and a branchless push: the child refs
+                    // are always consumed, so the compiler cannot defer their load behind
+                    // the box test (which cost a second dependent memory round trip).
+                    const DNode nd = load_node(sc.nodes + (cur & GS_REF_MASK));
                     c_nodes++;
-                    if (box_hit(nd, ray.o, inv, tmin, closest)) {
-                        if (nd.right != GS_REF_NONE) {
-                            s_stack[sp * GS_BLOCK + tid] = nd.right;
-                            sp++;
-                        }
-                        cur = nd.left;
-                    } else {
-                        cur = GS_REF_NONE;
-                    }
+                    const bool h = box_hit(nd, ray.o, inv, tmin, closest);
+                    s_stack[sp * GS_BLOCK + tid] = nd.right;  // in bounds: sp < BVH depth here
+                    sp += (h && nd.right != GS_REF_NONE) ? 1u : 0u;
+                    cur = h ? nd.left : (uint32_t)GS_REF_NONE;
                 } else if (kind == GS_REF_SPHERE) {
                     c_sph++;
                     const DSphere s = sc.spheres[cur & GS_REF_MASK];
@@ -824,7 +839,7 @@ __global__ void gs_unpack_kernel(const float* __restrict__ in, float* __restrict
 
 // =============================================================== host side
 static thread_local std::string tl_err;
-static int32_t g_shade_batch = 32;
+static int32_t g_shade_batch = 60;  // swept on MI355X C4: 32 -> 1459, 56 -> 1603, 60 -> 1623, 64 -> 1564 Msamples/s
 static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
 
 extern "C" void gs_set_last_error(const char* msg) { tl_err = msg ? msg : ""; }
