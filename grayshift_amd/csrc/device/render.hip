@@ -83,17 +83,30 @@ struct DevScene {
     uint32_t root;
 };
 
-struct KArgs {
+// Cold launch parameters: written to device memory per launch and read through a
+// pointer at their (conditional) use sites, so they are not hoisted into SGPRs for
+// the whole kernel (a by-value struct of this size spilled SGPRs into VGPR lanes,
+// costing 16 v_readlane per traversal step).
+struct KParams {
     DevScene sc;
     gs_camera cam;
     gs_sample_settings ss;
     uint64_t seed;
-    int32_t rank, world_size, tile_w, tile_h, tiles_x, shade_batch;
-    uint32_t capacity;
+    int32_t rank, world_size, tile_w, tile_h, tiles_x, pad;
+    uint32_t capacity, pad2;
     float* out;
     unsigned long long* counters;
     uint32_t* queue;
     uint32_t* item_visits;  // diagnostic: node visits per packed pixel (nullable)
+};
+
+// Hot kernel arguments: what the traversal loop reads every step.
+struct KArgs {
+    const DNode* nodes;
+    const DSphere* spheres;
+    const KParams* P;
+    uint32_t root;
+    int32_t shade_batch;
 };
 
 enum { S_NEED = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };
@@ -541,15 +554,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     if (threadIdx.x < C_N) s_cnt[threadIdx.x] = 0;
     __syncthreads();
 
-    const DevScene& sc = A.sc;
-    const gs_camera& cam = A.cam;
+    const KParams* __restrict__ P = A.P;
+    const DevScene& sc = P->sc;
+    const gs_camera& cam = P->cam;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t tid = threadIdx.x;
     const double tmin = 0.001;
-    const uint32_t tile_px = (uint32_t)(A.tile_w * A.tile_h);
-    const bool blocked8 = (A.tile_w % 8 == 0) && (A.tile_h % 8 == 0);
-    const double confidence_sq = A.ss.confidence * A.ss.confidence;
-    const double tolerance_sq = A.ss.tolerance * A.ss.tolerance;
 #define LD(k) s_d[(k) * GS_BLOCK + tid]
 #define LI(k) s_i[(k) * GS_BLOCK + tid]
 
@@ -572,7 +582,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 
     auto begin_ray = [&]() {
         inv = mk(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
-        cur = sc.root;
+        cur = A.root;
         sp = 0;
         closest = 1.7976931348623157e308;  // f64::MAX (camera.rs:177)
         hit_ref = GS_REF_NONE;
@@ -600,19 +610,21 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             if (LI(L_BLEFT) == 0) {
                 // end of a batch (camera.rs:149-164)
                 const double scount = LD(L_SCOUNT), lsum = LD(L_LSUM), lsq = LD(L_LSQ);
+                const double confidence_sq = P->ss.confidence * P->ss.confidence;
+                const double tolerance_sq = P->ss.tolerance * P->ss.tolerance;
                 double mean = lsum / scount;
                 double variance_sq = 1.0 / (scount - 1.0) * (lsq - lsum * lsum / scount);
                 double convergence_sq = confidence_sq * variance_sq / scount;
                 bool stop = convergence_sq < (mean * mean * tolerance_sq);
-                if (!stop) stop = (uint32_t)sat_u64(scount, 4294967295.0, 4294967295ull) > A.ss.max_samples;
+                if (!stop) stop = (uint32_t)sat_u64(scount, 4294967295.0, 4294967295ull) > P->ss.max_samples;
                 if (stop) {
                     const uint32_t item = LI(L_ITEM);
-                    float* o = A.out + (size_t)item * 3;
+                    float* o = P->out + (size_t)item * 3;
                     o[0] = (float)(LD(L_CSR) / scount);
                     o[1] = (float)(LD(L_CSG) / scount);
                     o[2] = (float)(LD(L_CSB) / scount);
                     atomicAdd(&s_cnt[C_PIX], 1ull);
-                    if (A.item_visits) A.item_visits[item] = c_nodes;
+                    if (P->item_visits) P->item_visits[item] = c_nodes;
                     atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
                     atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
                     c_nodes = 0;
@@ -620,13 +632,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     st = S_NEED;
                     return;
                 }
-                LD(L_SCOUNT) = scount + (double)A.ss.batch_size;
-                LI(L_BLEFT) = A.ss.batch_size;
+                LD(L_SCOUNT) = scount + (double)P->ss.batch_size;
+                LI(L_BLEFT) = P->ss.batch_size;
             }
             // Camera::get_ray (camera.rs:204-221) on the seeded stream of this sample
             const uint32_t pix = LI(L_PIX);
             const uint32_t pi = pix % (uint32_t)cam.image_width, pj = pix / (uint32_t)cam.image_width;
-            rng = stream_seed(A.seed, pix, sample);
+            rng = stream_seed(P->seed, pix, sample);
             atomicAdd(&s_cnt[C_PATHS], 1ull);
             double offx = wy_f64(rng) - 0.5;
             double offy = wy_f64(rng) - 0.5;
@@ -669,31 +681,33 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             const uint32_t n = (uint32_t)__popcll(need);
             const uint32_t leader = (uint32_t)__ffsll((long long)need) - 1;
             uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(A.queue, n);
+            if (lane == leader) base = atomicAdd(P->queue, n);
             base = __shfl(base, leader);
-            if ((uint64_t)base + n >= (uint64_t)A.capacity) qdone = true;
+            const uint32_t tile_px = (uint32_t)(P->tile_w * P->tile_h);
+            const bool blocked8 = (P->tile_w % 8 == 0) && (P->tile_h % 8 == 0);
+            if ((uint64_t)base + n >= (uint64_t)P->capacity) qdone = true;
             if (st == S_NEED) {
                 const uint64_t q = (uint64_t)base + (uint64_t)__popcll(need & lanemask_lt(lane));
-                if (q >= A.capacity) {
+                if (q >= P->capacity) {
                     st = S_DONE;
                 } else {
                     // work order: 8x8 blocks inside each tile (coherent primary rays)
                     const uint32_t slot = (uint32_t)(q / tile_px), w = (uint32_t)(q % tile_px);
                     uint32_t x, y;
                     if (blocked8) {
-                        const uint32_t b = w >> 6, l = w & 63, bpr = (uint32_t)A.tile_w >> 3;
+                        const uint32_t b = w >> 6, l = w & 63, bpr = (uint32_t)P->tile_w >> 3;
                         x = (b % bpr) * 8 + (l & 7);
                         y = (b / bpr) * 8 + (l >> 3);
                     } else {
-                        x = w % (uint32_t)A.tile_w;
-                        y = w / (uint32_t)A.tile_w;
+                        x = w % (uint32_t)P->tile_w;
+                        y = w / (uint32_t)P->tile_w;
                     }
-                    const uint32_t item = slot * tile_px + y * (uint32_t)A.tile_w + x;
-                    const uint32_t tile = (uint32_t)A.rank + slot * (uint32_t)A.world_size;
-                    const uint32_t pi = (tile % (uint32_t)A.tiles_x) * (uint32_t)A.tile_w + x;
-                    const uint32_t pj = (tile / (uint32_t)A.tiles_x) * (uint32_t)A.tile_h + y;
+                    const uint32_t item = slot * tile_px + y * (uint32_t)P->tile_w + x;
+                    const uint32_t tile = (uint32_t)P->rank + slot * (uint32_t)P->world_size;
+                    const uint32_t pi = (tile % (uint32_t)P->tiles_x) * (uint32_t)P->tile_w + x;
+                    const uint32_t pj = (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + y;
                     if (pi >= (uint32_t)cam.image_width || pj >= (uint32_t)cam.image_height) {
-                        float* o = A.out + (size_t)item * 3;  // padding pixel
+                        float* o = P->out + (size_t)item * 3;  // padding pixel
                         o[0] = 0.0f;
                         o[1] = 0.0f;
                         o[2] = 0.0f;
@@ -706,8 +720,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         LD(L_LSUM) = 0.0;
                         LD(L_LSQ) = 0.0;
                         // first batch starts (camera.rs:137)
-                        LD(L_SCOUNT) = 0.0 + (double)A.ss.batch_size;
-                        LI(L_BLEFT) = A.ss.batch_size;
+                        LD(L_SCOUNT) = 0.0 + (double)P->ss.batch_size;
+                        LI(L_BLEFT) = P->ss.batch_size;
                         sample = 0;
                         advance();
                     }
@@ -730,7 +744,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     // All 64 B in one go (4 x dwordx4) and a branchless push: the child refs
                     // are always consumed, so the compiler cannot defer their load behind
                     // the box test (which cost a second dependent memory round trip).
-                    const DNode nd = load_node(sc.nodes + (cur & GS_REF_MASK));
+                    const DNode nd = load_node(A.nodes + (cur & GS_REF_MASK));
                     c_nodes++;
                     const bool h = box_hit(nd, ray.o, inv, tmin, closest);
                     s_stack[sp * GS_BLOCK + tid] = nd.right;  // in bounds: sp < BVH depth here
@@ -738,7 +752,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     cur = h ? nd.left : (uint32_t)GS_REF_NONE;
                 } else if (kind == GS_REF_SPHERE) {
                     c_sph++;
-                    const DSphere s = sc.spheres[cur & GS_REF_MASK];
+                    const DSphere s = A.spheres[cur & GS_REF_MASK];
                     double t;
                     if (sphere_accept(mk(s.cx, s.cy, s.cz), s.r, ray, len2(ray.d), tmin, closest, t)) {
                         closest = t;
@@ -813,7 +827,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
     atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
     __syncthreads();
-    if (threadIdx.x < C_N && A.counters) atomicAdd(&A.counters[threadIdx.x], s_cnt[threadIdx.x]);
+    if (threadIdx.x < C_N && P->counters) atomicAdd(&P->counters[threadIdx.x], s_cnt[threadIdx.x]);
 }
 
 // Scatter rank-packed tiles into the frame.
@@ -858,6 +872,7 @@ struct gs_device_scene {
     void* mem = nullptr;  // one allocation for every array
     size_t bytes = 0;
     uint32_t* queue = nullptr;
+    KParams* params = nullptr;  // per-launch cold parameters (device memory)
     DevScene dev{};
     uint32_t n_nodes = 0;
     uint32_t stack_depth = 1;  // LDS stack entries per lane (= BVH depth)
@@ -1051,6 +1066,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     size_t o_texel = L.add(s->texels8, s->n_texels8);
     size_t o_hdri = L.add(s->hdri_rgb, s->background.kind == GS_BG_HDRI ? s->n_hdri_floats * 4 : 0);
     size_t o_queue = L.add(nullptr, 64);
+    size_t o_params = L.add(nullptr, sizeof(KParams));
 
     auto ds = new gs_device_scene();
     (void)hipGetDevice(&ds->device);
@@ -1084,6 +1100,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     d.bg = s->background;
     d.root = s->root;
     ds->queue = (uint32_t*)(b + o_queue);
+    ds->params = (KParams*)(b + o_params);
     ds->n_nodes = s->n_nodes;
     ds->stack_depth = depth < 1 ? 1 : depth;
     *out = ds;
@@ -1132,22 +1149,29 @@ gs_status gs_render_tiles_debug_async(const gs_device_scene* ds, const gs_camera
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
     if (dev != ds->device) return fail(GS_ERR_ARG, "scene lives on another device");
+    KParams kp{};
+    kp.sc = ds->dev;
+    kp.cam = *cam;
+    kp.ss = *ss;
+    kp.seed = seed;
+    kp.rank = part->rank;
+    kp.world_size = part->world_size;
+    kp.tile_w = part->tile_w;
+    kp.tile_h = part->tile_h;
+    kp.tiles_x = (cam->image_width + part->tile_w - 1) / part->tile_w;
+    kp.capacity = (uint32_t)cap;
+    kp.out = d_out;
+    kp.counters = (unsigned long long*)d_counters;
+    kp.queue = ds->queue;
+    kp.item_visits = d_item_visits;
     KArgs a{};
-    a.sc = ds->dev;
-    a.cam = *cam;
-    a.ss = *ss;
-    a.seed = seed;
-    a.rank = part->rank;
-    a.world_size = part->world_size;
-    a.tile_w = part->tile_w;
-    a.tile_h = part->tile_h;
-    a.tiles_x = (cam->image_width + part->tile_w - 1) / part->tile_w;
+    a.nodes = ds->dev.nodes;
+    a.spheres = ds->dev.spheres;
+    a.P = ds->params;
+    a.root = ds->dev.root;
     a.shade_batch = g_shade_batch;
-    a.capacity = (uint32_t)cap;
-    a.out = d_out;
-    a.counters = (unsigned long long*)d_counters;
-    a.queue = ds->queue;
-    a.item_visits = d_item_visits;
+    // Pageable source: the runtime stages it before returning, so `kp` may go out of scope.
+    HIPCHK(hipMemcpyAsync(ds->params, &kp, sizeof(KParams), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(ds->queue, 0, 4, st));
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
