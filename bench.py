@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--cpu-stride", type=int, default=4, help="CPU baseline: every Nth row and column")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch (profiles/)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_C4_latest.json"),
+                    help="JSON with PMC-derived HBM bytes per launch (tools/pmc.sh -> profiles/)")
     ap.add_argument("--dump", default=None, help="write the frame (rank 0) as .npy")
     return ap.parse_args()
 
@@ -151,7 +152,7 @@ def main():
     if a.traffic and os.path.exists(a.traffic):
         with open(a.traffic) as f:
             tj = json.load(f)
-        if tj.get("config") == a.config and tj.get("hbm_bytes_per_launch"):
+        if tj.get("config") == a.config and tj.get("hbm_bytes_per_launch") and a.width is None and a.spp is None:
             traffic = tj["hbm_bytes_per_launch"]
 
     if rank == 0:

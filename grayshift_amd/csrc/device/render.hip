@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cmath>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -56,10 +57,24 @@ struct alignas(16) DNode {  // 64 B: box (f64, as AABB.rs) + children
 struct alignas(16) DSphere {  // 32 B: what Sphere::hit reads; material kept apart
     double cx, cy, cz, r;
 };
+// Material record with the common texture cases folded in (64 B, one line): a
+// Lambertian/DiffuseLight over a SolidColorTexture, or over a CheckeredTexture of two
+// solids (the bouncing_spheres ground), reads no texture record at shading time.
+enum {
+    DM_LAMB_SOLID = 1,    // a = albedo
+    DM_LAMB_CHECKER = 2,  // a = even, b = odd, param = scale_inv   (texture.rs:58-70)
+    DM_LAMB_TEX = 3,      // generic texture tree: `texture`
+    DM_METAL = 4,         // a = albedo, param = fuzz
+    DM_DIELECTRIC = 5,    // param = refraction index
+    DM_LIGHT_SOLID = 6,   // a = emitted colour
+    DM_LIGHT_TEX = 7      // `texture`
+};
 struct alignas(16) DMaterial {
     uint32_t kind, texture, needs_uv, pad;
-    double albedo[3];
+    double a[3];
     double param;
+    double b[3];
+    double pad2;
 };
 
 enum { C_RAYS = 0, C_NODES, C_SPH, C_MSPH, C_QUAD, C_TRI, C_INST, C_LIST, C_HITS, C_IMG, C_HDRI, C_PATHS, C_PIX, C_N };
@@ -79,6 +94,7 @@ struct DevScene {
     const gs_image* images;
     const uint8_t* texels;
     const float* hdri;
+    const uint32_t* hdri_rgbe;  // non-null when every texel round-trips through RGBE8
     gs_background bg;
     uint32_t root;
 };
@@ -450,8 +466,17 @@ __device__ GS_NOINLINE d3 background(const DevScene& sc, d3 dir, unsigned long l
     double v = 0.5 - phi / PI;
     uint64_t x = sat_u64(u * (double)bg.width, 18446744073709551616.0, ~0ull) % (uint64_t)bg.width;
     uint64_t y = sat_u64(v * (double)bg.height, 18446744073709551616.0, ~0ull) % (uint64_t)bg.height;
-    const float* px = sc.hdri + (y * (uint64_t)bg.width + x) * 3;
+    const uint64_t k = y * (uint64_t)bg.width + x;
     atomicAdd(&cnt[C_HDRI], 1ull);
+    if (sc.hdri_rgbe) {
+        // RGBE8 texel (4 B): m * 2^(e-136) is exactly the f32 radiant produced, so the
+        // f64 value equals the reference's `color.r as f64` (verified per texel at upload).
+        const uint32_t t = sc.hdri_rgbe[k];
+        const uint32_t e = t >> 24;
+        const double sc2 = e ? ldexp(1.0, (int)e - 136) : 0.0;
+        return mk((double)(t & 0xffu) * sc2, (double)((t >> 8) & 0xffu) * sc2, (double)((t >> 16) & 0xffu) * sc2);
+    }
+    const float* px = sc.hdri + k * 3;
     return mk((double)px[0], (double)px[1], (double)px[2]);
 }
 
@@ -477,6 +502,14 @@ struct Scatter {
     uint32_t cont;
 };
 
+__device__ __forceinline__ d3 checker(const DMaterial& m, d3 p) {  // texture.rs:58-70
+    int32_t xi = sat_i32(floor(m.param * p.x));
+    int32_t yi = sat_i32(floor(m.param * p.y));
+    int32_t zi = sat_i32(floor(m.param * p.z));
+    int32_t s = (int32_t)((uint32_t)xi + (uint32_t)yi + (uint32_t)zi);
+    return (s % 2 == 0) ? ld3(m.a) : ld3(m.b);
+}
+
 __device__ GS_NOINLINE Scatter scatter(const DevScene& sc, HitRec h, d3 in_dir, uint64_t rng,
                                         unsigned long long* cnt) {
     const DMaterial& m = sc.mats[h.mat];
@@ -484,8 +517,11 @@ __device__ GS_NOINLINE Scatter scatter(const DevScene& sc, HitRec h, d3 in_dir, 
     s.cont = 0;
     s.col = mk(0.0, 0.0, 0.0);
     s.dir = mk(0.0, 0.0, 0.0);
-    if (m.kind == GS_MAT_LAMBERTIAN) {  // :45-68
-        s.col = texture_value(sc, m.texture, h.u, h.v, h.p, cnt);
+    const uint32_t kind = m.kind;
+    if (kind <= DM_LAMB_TEX) {  // Lambertian :45-68
+        s.col = kind == DM_LAMB_SOLID ? ld3(m.a)
+              : kind == DM_LAMB_CHECKER ? checker(m, h.p)
+                                        : texture_value(sc, m.texture, h.u, h.v, h.p, cnt);
         // OrthonormalBasis::new (ONB.rs:10-23)
         d3 w = unit(h.n);
         d3 a = fabs(w.x) > 0.9 ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);
@@ -503,15 +539,15 @@ __device__ GS_NOINLINE Scatter scatter(const DevScene& sc, HitRec h, d3 in_dir, 
         d3 cd = mk(cp * q, sp * q, sqrt(1.0 - r2));
         s.dir = unit(add(add(muls(uu, cd.x), muls(vv, cd.y)), muls(w, cd.z)));
         s.cont = 1;
-    } else if (m.kind == GS_MAT_METAL) {  // :87-102
+    } else if (kind == DM_METAL) {  // :87-102
         d3 reflected = reflect(in_dir, h.n);
         reflected = add(unit(reflected), muls(random_unit_vector(rng), m.param));
         if (dot(reflected, h.n) > 0.0) {
-            s.col = ld3(m.albedo);
+            s.col = ld3(m.a);
             s.dir = reflected;
             s.cont = 1;
         }
-    } else if (m.kind == GS_MAT_DIELECTRIC) {  // :123-148
+    } else if (kind == DM_DIELECTRIC) {  // :123-148
         double ri = h.front ? 1.0 / m.param : m.param;
         d3 ud = unit(in_dir);
         double cos_theta = fmin(dot(neg(ud), h.n), 1.0);
@@ -527,8 +563,8 @@ __device__ GS_NOINLINE Scatter scatter(const DevScene& sc, HitRec h, d3 in_dir, 
         s.dir = (cannot_refract || fresnel) ? reflect(ud, h.n) : refract(ud, h.n, ri);
         s.col = mk(1.0, 1.0, 1.0);
         s.cont = 1;
-    } else if (m.kind == GS_MAT_DIFFUSE_LIGHT) {  // :165-169 (emits, never scatters)
-        s.col = texture_value(sc, m.texture, h.u, h.v, h.p, cnt);
+    } else {  // DiffuseLight :165-169 (emits, never scatters)
+        s.col = kind == DM_LIGHT_SOLID ? ld3(m.a) : texture_value(sc, m.texture, h.u, h.v, h.p, cnt);
     }
     s.rng = rng;
     return s;
@@ -994,6 +1030,37 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out) {
     return GS_OK;
 }
 
+// f32 RGB -> RGBE8 (shared exponent), accepted only if m * 2^(e-136) reproduces all
+// three floats exactly (true for texels that came from an RGBE file, as airport.hdr's).
+bool encode_rgbe(const float* c, uint32_t* out) {
+    const float r = c[0], g = c[1], b = c[2];
+    if (!(r >= 0.0f && g >= 0.0f && b >= 0.0f)) return false;
+    if (std::signbit(r) || std::signbit(g) || std::signbit(b)) return false;
+    const float mx = std::fmax(r, std::fmax(g, b));
+    if (mx == 0.0f) {
+        *out = 0;
+        return true;
+    }
+    int ex = 0;
+    std::frexp((double)mx, &ex);
+    for (int e = ex + 128; e >= 1 && e >= ex + 120; e--) {  // try the canonical exponent first
+        if (e > 255) continue;
+        const double scale = std::ldexp(1.0, e - 136);
+        uint32_t m[3];
+        bool ok = true;
+        for (int k = 0; k < 3 && ok; k++) {
+            const double q = (double)c[k] / scale;
+            ok = q >= 0.0 && q <= 255.0 && q == std::floor(q) && (float)(q * scale) == c[k];
+            m[k] = ok ? (uint32_t)q : 0;
+        }
+        if (ok) {
+            *out = m[0] | (m[1] << 8) | (m[2] << 16) | ((uint32_t)e << 24);
+            return true;
+        }
+    }
+    return false;
+}
+
 // Does the texture tree under `t` contain an image (=> sphere uv must be computed)?
 bool tex_needs_uv(const gs_flat_scene& s, uint32_t t, int depth = 0) {
     if (t >= s.n_textures || depth > 16) return false;
@@ -1043,12 +1110,45 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     for (uint32_t i = 0; i < s->n_materials; i++) {
         const gs_material& m = s->materials[i];
         DMaterial d{};
-        d.kind = m.kind;
         d.texture = m.texture;
-        d.needs_uv = (m.kind == GS_MAT_LAMBERTIAN || m.kind == GS_MAT_DIFFUSE_LIGHT) ? tex_needs_uv(*s, m.texture) : 0;
-        for (int k = 0; k < 3; k++) d.albedo[k] = m.albedo[k];
-        d.param = m.param;
+        const bool textured = m.kind == GS_MAT_LAMBERTIAN || m.kind == GS_MAT_DIFFUSE_LIGHT;
+        d.needs_uv = textured ? tex_needs_uv(*s, m.texture) : 0;
+        if (textured) {
+            const gs_texture& t = s->textures[m.texture];
+            const bool solid = t.kind == GS_TEX_SOLID;
+            const bool checker2 = t.kind == GS_TEX_CHECKERED && s->textures[t.even].kind == GS_TEX_SOLID &&
+                                  s->textures[t.odd].kind == GS_TEX_SOLID;
+            if (m.kind == GS_MAT_LAMBERTIAN) {
+                d.kind = solid ? DM_LAMB_SOLID : (checker2 ? DM_LAMB_CHECKER : DM_LAMB_TEX);
+            } else {
+                d.kind = solid ? DM_LIGHT_SOLID : DM_LIGHT_TEX;
+            }
+            if (solid) {
+                for (int k = 0; k < 3; k++) d.a[k] = t.color[k];
+            } else if (checker2 && m.kind == GS_MAT_LAMBERTIAN) {
+                for (int k = 0; k < 3; k++) {
+                    d.a[k] = s->textures[t.even].color[k];
+                    d.b[k] = s->textures[t.odd].color[k];
+                }
+                d.param = t.scale_inv;
+            }
+        } else if (m.kind == GS_MAT_METAL) {
+            d.kind = DM_METAL;
+            for (int k = 0; k < 3; k++) d.a[k] = m.albedo[k];
+            d.param = m.param;
+        } else {
+            d.kind = DM_DIELECTRIC;
+            d.param = m.param;
+        }
         mats[i] = d;
+    }
+    // HDRI: keep 4-byte RGBE texels when every f32 texel round-trips exactly.
+    std::vector<uint32_t> rgbe;
+    if (s->background.kind == GS_BG_HDRI) {
+        const uint64_t n = (uint64_t)s->background.width * s->background.height;
+        rgbe.resize(n);
+        for (uint64_t k = 0; k < n && !rgbe.empty(); k++)
+            if (!encode_rgbe(s->hdri_rgb + 3 * k, &rgbe[k])) rgbe.clear();
     }
     Layout L;
     size_t o_nodes = L.add(nodes.data(), nodes.size() * sizeof(DNode));
@@ -1064,7 +1164,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     size_t o_tex = L.add(s->textures, s->n_textures * sizeof(gs_texture));
     size_t o_img = L.add(s->images, s->n_images * sizeof(gs_image));
     size_t o_texel = L.add(s->texels8, s->n_texels8);
-    size_t o_hdri = L.add(s->hdri_rgb, s->background.kind == GS_BG_HDRI ? s->n_hdri_floats * 4 : 0);
+    size_t o_hdri = L.add(s->hdri_rgb, (s->background.kind == GS_BG_HDRI && rgbe.empty()) ? s->n_hdri_floats * 4 : 0);
+    size_t o_rgbe = L.add(rgbe.data(), rgbe.size() * 4);
     size_t o_queue = L.add(nullptr, 64);
     size_t o_params = L.add(nullptr, sizeof(KParams));
 
@@ -1097,6 +1198,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     d.images = (const gs_image*)(b + o_img);
     d.texels = (const uint8_t*)(b + o_texel);
     d.hdri = (const float*)(b + o_hdri);
+    d.hdri_rgbe = rgbe.empty() ? nullptr : (const uint32_t*)(b + o_rgbe);
     d.bg = s->background;
     d.root = s->root;
     ds->queue = (uint32_t*)(b + o_queue);
