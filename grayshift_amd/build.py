@@ -29,6 +29,7 @@ SOURCES = [
 ]
 DEPS = SOURCES + [
     os.path.join(HERE, "csrc", "device", "devmath.hpp"),
+    os.path.join(HERE, "csrc", "device", "geometry.hpp"),
     os.path.join(HERE, "csrc", "host", "world.hpp"),
     os.path.join(ROOT, "include", "grayshift_gpu.h"),
     os.path.join(ROOT, "include", "grayshift_host.h"),
@@ -75,6 +76,23 @@ def build_product(force=False, verbose=False, extra=(), out=None):
     return lib
 
 
+KAT_SRC = os.path.join(ROOT, "tests", "hip", "kat_device.hip")
+KAT_LIB = os.path.join(ROOT, "tests", "hip", "libkat_device.so")
+
+
+def build_kat(force=False, verbose=False):
+    """Test-only HIP harness running the kernel's device functions on test arrays."""
+    deps = [KAT_SRC] + DEPS
+    if not force and not _stale(KAT_LIB, deps):
+        return KAT_LIB
+    cmd = [HIPCC] + COMMON + ["-x", "hip", "--offload-arch=" + ARCH, "-shared", "-o", KAT_LIB + ".tmp", KAT_SRC]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(KAT_LIB + ".tmp", KAT_LIB)
+    return KAT_LIB
+
+
 def build_oracle(force=False, verbose=False):
     if force and os.path.exists(ORACLE_LIB):
         os.remove(ORACLE_LIB)
@@ -103,6 +121,7 @@ def main(argv=None):
         print("variant", path, flags)
     if not a.no_oracle:
         build_oracle(force=a.force, verbose=a.verbose)
+        build_kat(force=a.force, verbose=a.verbose)
     print("built", LIB, "" if a.no_oracle else ORACLE_LIB)
 
 

@@ -1,0 +1,139 @@
+// geometry.hpp — device-side restatements of the reference's geometric tests
+// (AABB.rs, sphere.rs, quad.rs/plane.rs, triangle.rs, hittable.rs Translate/RotateY)
+// and the device records they read.  Shared by the megakernel (render.hip) and the
+// device known-answer-test harness (tests/hip/kat_device.hip).
+#pragma once
+#include "../../../include/grayshift_gpu.h"
+#include "devmath.hpp"
+
+namespace gsd {
+
+struct alignas(16) DNode {  // 64 B: box (f64, as AABB.rs) + children
+    double mnx, mny, mnz, mxx, mxy, mxz;
+    uint32_t left, right, pad0, pad1;
+};
+struct alignas(16) DSphere {  // 32 B: what Sphere::hit reads; material kept apart
+    double cx, cy, cz, r;
+};
+struct Ray {
+    d3 o, d;
+    double time;
+};
+
+__device__ __forceinline__ DNode load_node(const DNode* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+    DNode n;
+    n.mnx = __hiloint2double((int)a.y, (int)a.x);
+    n.mny = __hiloint2double((int)a.w, (int)a.z);
+    n.mnz = __hiloint2double((int)b.y, (int)b.x);
+    n.mxx = __hiloint2double((int)b.w, (int)b.z);
+    n.mxy = __hiloint2double((int)c.y, (int)c.x);
+    n.mxz = __hiloint2double((int)c.w, (int)c.z);
+    n.left = d.x;
+    n.right = d.y;
+    n.pad0 = d.z;
+    n.pad1 = d.w;
+    return n;
+}
+
+// AABB::hit (AABB.rs:58-113) with the reference's 1.0/d hoisted per ray (same value).
+// The early-outs of the reference do not change the boolean: once max <= min the
+// later slabs only raise min / lower max, and NaN slabs never assign.
+// `if a > lo { lo = a }` == fmax(lo, a) because lo is never NaN (tmin / tmax and only
+// non-NaN values are ever assigned) and IEEE maxNum ignores a NaN operand, as the
+// reference's failed comparison does (a == lo keeps an equal value).  Same for hi.
+// The t0/t1 swap must stay a compare-select: min/max would treat a NaN t1 differently.
+__device__ __forceinline__ void slab(double mn, double mx, double o, double inv, double& lo, double& hi) {
+    const double t0 = (mn - o) * inv, t1 = (mx - o) * inv;
+    const bool s = t0 < t1;
+    const double a = s ? t0 : t1, b = s ? t1 : t0;
+    lo = fmax(lo, a);
+    hi = fmin(hi, b);
+}
+__device__ __forceinline__ bool box_hit(const DNode& n, const d3& o, const d3& inv, double tmin, double tmax) {
+    double lo = tmin, hi = tmax;
+    slab(n.mnx, n.mxx, o.x, inv.x, lo, hi);
+    slab(n.mny, n.mxy, o.y, inv.y, lo, hi);
+    slab(n.mnz, n.mxz, o.z, inv.z, lo, hi);
+    return !(hi <= lo);
+}
+
+// Sphere::hit acceptance (sphere.rs:64-88): returns t or a NaN-free miss flag.
+__device__ __forceinline__ bool sphere_accept(d3 c, double r, const Ray& ray, double a, double tmin, double tmax,
+                                         double& t_out) {
+    d3 oc = sub(c, ray.o);
+    double h = dot(ray.d, oc);
+    double cc = len2(oc) - r * r;
+    double disc = h * h - a * cc;
+    if (disc < 0.0) return false;
+    double sq = sqrt(disc);
+    double t = (h - sq) / a;
+    if (!(tmin < t && t < tmax)) {
+        t = (h + sq) / a;
+        if (!(tmin < t && t < tmax)) return false;
+    }
+    t_out = t;
+    return true;
+}
+
+// Quad::hit acceptance (quad.rs:84-95, plane.rs:20-32).
+__device__ __forceinline__ bool quad_accept(const gs_quad& q, const Ray& ray, double tmin, double tmax, double& t_out) {
+    d3 nrm = ld3(q.normal);
+    double den = dot(nrm, ray.d);
+    if (fabs(den) < 1e-8) return false;
+    double t = (q.d - dot(nrm, ray.o)) / den;
+    if (!(tmin <= t && t <= tmax)) return false;
+    d3 inter = add(ray.o, muls(ray.d, t));
+    d3 planar = sub(inter, ld3(q.q));
+    double alpha = dot(ld3(q.w), cross(planar, ld3(q.v)));
+    double beta = dot(ld3(q.w), cross(ld3(q.u), planar));
+    if (!(0.0 <= alpha && alpha <= 1.0) || !(0.0 <= beta && beta <= 1.0)) return false;
+    t_out = t;
+    return true;
+}
+
+// Triangle::hit (triangle.rs:34-68): one-sided, ray_t ignored (reference quirk).
+__device__ __forceinline__ bool tri_hit(const gs_triangle& tr, const Ray& ray, double& t_out, double& u_out,
+                                        double& v_out) {
+    d3 a = ld3(tr.a);
+    d3 e1 = sub(ld3(tr.c), a), e2 = sub(ld3(tr.b), a);
+    d3 p_vec = cross(ray.d, e2);
+    double det = dot(e1, p_vec);
+    if (det < 1e-8) return false;
+    d3 t_vec = sub(ray.o, a);
+    double u = dot(t_vec, p_vec);
+    if (u < 0.0 || u > det) return false;
+    d3 q_vec = cross(t_vec, e1);
+    double v = dot(ray.d, q_vec);
+    if (v < 0.0 || u + v > det) return false;
+    double t = dot(e2, q_vec);
+    double inv_det = 1.0 / det;
+    t_out = t * inv_det;
+    u_out = u * inv_det;
+    v_out = v * inv_det;
+    return true;
+}
+
+// Translate/RotateY forward ray transforms (hittable.rs:107-113, :179-193).
+__device__ __forceinline__ void inst_forward(const gs_instance& in, Ray& r) {
+    if (in.kind == GS_INST_TRANSLATE) {
+        r.o = sub(r.o, ld3(in.p));
+    } else {
+        double s = in.p[0], c = in.p[1];
+        r.o = mk((c * r.o.x) - (s * r.o.z), r.o.y, (s * r.o.x) + (c * r.o.z));
+        r.d = mk((c * r.d.x) - (s * r.d.z), r.d.y, (s * r.d.x) + (c * r.d.z));
+    }
+}
+// Hit-record back transforms (hittable.rs:115-117, :195-207).
+__device__ __forceinline__ void inst_backward(const gs_instance& in, d3& p, d3& n) {
+    if (in.kind == GS_INST_TRANSLATE) {
+        p = add(p, ld3(in.p));
+    } else {
+        double s = in.p[0], c = in.p[1];
+        p = mk((c * p.x) + (s * p.z), p.y, (-s * p.x) + (c * p.z));
+        n = mk((c * n.x) + (s * n.z), n.y, (-s * n.x) + (c * n.z));
+    }
+}
+
+}  // namespace gsd

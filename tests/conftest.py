@@ -19,4 +19,5 @@ def built():
     from grayshift_amd import build
     build.build_product()
     build.build_oracle()
+    build.build_kat()
     return True

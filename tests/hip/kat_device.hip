@@ -1,0 +1,156 @@
+// kat_device.hip — TEST INFRASTRUCTURE: runs the megakernel's own device functions
+// (grayshift_amd/csrc/device/geometry.hpp, devmath.hpp) over arrays of test cases so
+// tests/test_gpu_device_kat.py can compare them bit-for-bit with the CPU oracle on
+// adversarial inputs (zero / negative-zero direction components, origins on slab
+// planes, tangent rays, closed/open interval ends).  Not part of the product.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../grayshift_amd/csrc/device/devmath.hpp"
+#include "../../grayshift_amd/csrc/device/geometry.hpp"
+
+using namespace gsd;
+
+__global__ void k_aabb(int n, const double* box, const double* ray, const double* iv, int* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    DNode nd{box[6 * i], box[6 * i + 1], box[6 * i + 2], box[6 * i + 3], box[6 * i + 4], box[6 * i + 5], 0, 0, 0, 0};
+    d3 o = mk(ray[6 * i], ray[6 * i + 1], ray[6 * i + 2]);
+    d3 d = mk(ray[6 * i + 3], ray[6 * i + 4], ray[6 * i + 5]);
+    d3 inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+    out[i] = box_hit(nd, o, inv, iv[2 * i], iv[2 * i + 1]) ? 1 : 0;
+}
+
+__global__ void k_sphere(int n, const double* sph, const double* ray, const double* iv, double* t, int* hit) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Ray r;
+    r.o = mk(ray[6 * i], ray[6 * i + 1], ray[6 * i + 2]);
+    r.d = mk(ray[6 * i + 3], ray[6 * i + 4], ray[6 * i + 5]);
+    r.time = 0.0;
+    double tt = 0.0;
+    bool h = sphere_accept(mk(sph[4 * i], sph[4 * i + 1], sph[4 * i + 2]), sph[4 * i + 3], r, len2(r.d), iv[2 * i],
+                           iv[2 * i + 1], tt);
+    hit[i] = h ? 1 : 0;
+    t[i] = tt;
+}
+
+__global__ void k_tri(int n, const double* tri, const double* ray, double* tuv, int* hit) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    gs_triangle g;
+    for (int k = 0; k < 3; k++) {
+        g.a[k] = tri[9 * i + k];
+        g.b[k] = tri[9 * i + 3 + k];
+        g.c[k] = tri[9 * i + 6 + k];
+    }
+    Ray r;
+    r.o = mk(ray[6 * i], ray[6 * i + 1], ray[6 * i + 2]);
+    r.d = mk(ray[6 * i + 3], ray[6 * i + 4], ray[6 * i + 5]);
+    r.time = 0.0;
+    double t = 0, u = 0, v = 0;
+    hit[i] = tri_hit(g, r, t, u, v) ? 1 : 0;
+    tuv[3 * i] = t;
+    tuv[3 * i + 1] = u;
+    tuv[3 * i + 2] = v;
+}
+
+__global__ void k_rng(int n, const uint64_t* seed, const uint32_t* pix, const uint32_t* smp, int draws, double* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t st = stream_seed(seed[i], pix[i], smp[i]);
+    for (int k = 0; k < draws; k++) out[(size_t)i * draws + k] = wy_f64(st);
+}
+
+// which: 0 sin, 1 cos, 2 acos, 3 asin, 4 atan2(x, y)
+__global__ void k_math(int n, int which, const double* x, const double* y, double* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double r;
+    if (which == 0) {
+        double s, c;
+        sincos(x[i], &s, &c);
+        r = s;
+    } else if (which == 1) {
+        double s, c;
+        sincos(x[i], &s, &c);
+        r = c;
+    } else if (which == 2) {
+        r = acos(x[i]);
+    } else if (which == 3) {
+        r = asin(x[i]);
+    } else {
+        r = atan2(x[i], y[i]);
+    }
+    out[i] = r;
+}
+
+template <class T>
+static T* dcopy(const T* h, size_t n) {
+    T* d = nullptr;
+    if (hipMalloc(&d, n * sizeof(T) + 8) != hipSuccess) return nullptr;
+    if (h) (void)hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice);
+    return d;
+}
+template <class T>
+static void back(T* h, T* d, size_t n) {
+    (void)hipMemcpy(h, d, n * sizeof(T), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+}
+static dim3 grid(int n) { return dim3((unsigned)((n + 255) / 256)); }
+
+extern "C" {
+
+int kat_aabb(int n, const double* box, const double* ray, const double* iv, int* out) {
+    double *db = dcopy(box, 6 * (size_t)n), *dr = dcopy(ray, 6 * (size_t)n), *di = dcopy(iv, 2 * (size_t)n);
+    int* dout = dcopy<int>(nullptr, n);
+    hipLaunchKernelGGL(k_aabb, grid(n), dim3(256), 0, 0, n, db, dr, di, dout);
+    back(out, dout, n);
+    (void)hipFree(db); (void)hipFree(dr); (void)hipFree(di);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+int kat_sphere(int n, const double* sph, const double* ray, const double* iv, double* t, int* hit) {
+    double *ds = dcopy(sph, 4 * (size_t)n), *dr = dcopy(ray, 6 * (size_t)n), *di = dcopy(iv, 2 * (size_t)n);
+    double* dt = dcopy<double>(nullptr, n);
+    int* dh = dcopy<int>(nullptr, n);
+    hipLaunchKernelGGL(k_sphere, grid(n), dim3(256), 0, 0, n, ds, dr, di, dt, dh);
+    back(t, dt, n);
+    back(hit, dh, n);
+    (void)hipFree(ds); (void)hipFree(dr); (void)hipFree(di);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+int kat_tri(int n, const double* tri, const double* ray, double* tuv, int* hit) {
+    double *dt = dcopy(tri, 9 * (size_t)n), *dr = dcopy(ray, 6 * (size_t)n);
+    double* dtuv = dcopy<double>(nullptr, 3 * (size_t)n);
+    int* dh = dcopy<int>(nullptr, n);
+    hipLaunchKernelGGL(k_tri, grid(n), dim3(256), 0, 0, n, dt, dr, dtuv, dh);
+    back(tuv, dtuv, 3 * (size_t)n);
+    back(hit, dh, n);
+    (void)hipFree(dt); (void)hipFree(dr);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+int kat_rng(int n, const uint64_t* seed, const uint32_t* pix, const uint32_t* smp, int draws, double* out) {
+    uint64_t* ds = dcopy(seed, n);
+    uint32_t *dp = dcopy(pix, n), *dm = dcopy(smp, n);
+    double* dout = dcopy<double>(nullptr, (size_t)n * draws);
+    hipLaunchKernelGGL(k_rng, grid(n), dim3(256), 0, 0, n, ds, dp, dm, draws, dout);
+    back(out, dout, (size_t)n * draws);
+    (void)hipFree(ds); (void)hipFree(dp); (void)hipFree(dm);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+int kat_math(int n, int which, const double* x, const double* y, double* out) {
+    double *dx = dcopy(x, n), *dy = dcopy(y ? y : x, n);
+    double* dout = dcopy<double>(nullptr, n);
+    hipLaunchKernelGGL(k_math, grid(n), dim3(256), 0, 0, n, which, dx, dy, dout);
+    back(out, dout, n);
+    (void)hipFree(dx); (void)hipFree(dy);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+}  // extern "C"
