@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--shade-batch", type=int, default=None)
     ap.add_argument("--blocks-per-cu", type=int, default=None)
+    ap.add_argument("--leaf-batch", type=int, default=None)
     ap.add_argument("--cpu-stride", type=int, default=4, help="CPU baseline: every Nth row and column")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
@@ -73,8 +74,8 @@ def main():
     import grayshift_amd as g
     from grayshift_amd import scenes
 
-    if a.shade_batch is not None or a.blocks_per_cu is not None:
-        g.set_tuning(a.shade_batch or 32, a.blocks_per_cu or 0)
+    if a.shade_batch is not None or a.blocks_per_cu is not None or a.leaf_batch is not None:
+        g.set_tuning(a.shade_batch or 60, a.blocks_per_cu or 0, a.leaf_batch or 0)
     sc = scenes.config(a.config, width=a.width, spp=a.spp)
     r = g.Renderer(sc, rank=rank, world_size=world, tile=a.tile)
     # Every rank's packed buffer has rank 0's capacity (round-robin gives it the most tiles)

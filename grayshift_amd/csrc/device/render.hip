@@ -117,6 +117,7 @@ struct KArgs {
     const KParams* P;
     uint32_t root;
     int32_t shade_batch;
+    int32_t leaf_batch;  // 0: test leaves in the same iteration as node steps (if-if)
 };
 
 enum { S_NEED = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };
@@ -640,9 +641,21 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             const uint64_t tr = __ballot(st == S_TRACE);
             if (tr == 0) break;
             if ((uint32_t)__popcll(__ballot(st == S_SHADE)) >= (uint32_t)A.shade_batch) break;
-            if (st == S_TRACE) {
-                const uint32_t kind = cur >> GS_REF_SHIFT;
-                if (kind == GS_REF_NODE) {
+            // Leaf batching: step nodes until `leaf_batch` tracing lanes sit at a leaf (or all
+            // do), then test those leaves together, so a wave pays for the node step and the
+            // sphere test in different iterations instead of both in every one.  Each lane
+            // still processes its refs in the reference's order.
+            const bool tracing = st == S_TRACE;
+            const bool at_leaf = tracing && (cur >> GS_REF_SHIFT) != GS_REF_NODE;
+            bool leaf_pass;
+            if (A.leaf_batch == 0) {
+                leaf_pass = at_leaf;  // if-if: both kinds every iteration
+            } else {
+                const uint64_t lm = __ballot(at_leaf);
+                leaf_pass = lm == tr || (uint32_t)__popcll(lm) >= (uint32_t)A.leaf_batch;
+            }
+            if (tracing) {
+                if (!at_leaf && (A.leaf_batch == 0 || !leaf_pass)) {
                     // All 64 B in one go (4 x dwordx4) and a branchless push: the child refs
                     // are always consumed, so the compiler cannot defer their load behind
                     // the box test (which cost a second dependent memory round trip).
@@ -652,22 +665,23 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     s_stack[sp * GS_BLOCK + tid] = nd.right;  // in bounds: sp < BVH depth here
                     sp += (h && nd.right != GS_REF_NONE) ? 1u : 0u;
                     cur = h ? nd.left : (uint32_t)GS_REF_NONE;
-                } else if (kind == GS_REF_SPHERE) {
-                    c_sph++;
-                    const DSphere s = A.spheres[cur & GS_REF_MASK];
-                    double t;
-                    if (sphere_accept(mk(s.cx, s.cy, s.cz), s.r, ray, len2(ray.d), tmin, closest, t)) {
-                        closest = t;
-                        hit_ref = cur;
-                        hit_inst = GS_REF_NONE;
-                    }
-                    cur = GS_REF_NONE;
-                } else {
-                    const LeafHit lh = leaf_other(sc, cur, ray, tmin, closest, s_cnt);
-                    if (lh.hit) {
-                        closest = lh.t;
-                        hit_ref = lh.ref;
-                        hit_inst = lh.inst;
+                } else if (at_leaf && leaf_pass) {
+                    if ((cur >> GS_REF_SHIFT) == GS_REF_SPHERE) {
+                        c_sph++;
+                        const DSphere s = A.spheres[cur & GS_REF_MASK];
+                        double t;
+                        if (sphere_accept(mk(s.cx, s.cy, s.cz), s.r, ray, len2(ray.d), tmin, closest, t)) {
+                            closest = t;
+                            hit_ref = cur;
+                            hit_inst = GS_REF_NONE;
+                        }
+                    } else {
+                        const LeafHit lh = leaf_other(sc, cur, ray, tmin, closest, s_cnt);
+                        if (lh.hit) {
+                            closest = lh.t;
+                            hit_ref = lh.ref;
+                            hit_inst = lh.inst;
+                        }
                     }
                     cur = GS_REF_NONE;
                 }
@@ -757,6 +771,7 @@ __global__ void gs_unpack_kernel(const float* __restrict__ in, float* __restrict
 static thread_local std::string tl_err;
 static int32_t g_shade_batch = 60;  // swept on MI355X C4: 32 -> 1459, 56 -> 1603, 60 -> 1623, 64 -> 1564 Msamples/s
 static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
+static int32_t g_leaf_batch = 0;
 
 extern "C" void gs_set_last_error(const char* msg) { tl_err = msg ? msg : ""; }
 static gs_status fail(gs_status code, const std::string& msg) {
@@ -943,9 +958,11 @@ extern "C" {
 const char* gs_last_error(void) { return tl_err.c_str(); }
 int32_t gs_version(void) { return GS_ABI_VERSION; }
 
-gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu) {
-    if (shade_batch < 1 || shade_batch > 64 || blocks_per_cu < 0 || blocks_per_cu > 8)
+gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf_batch) {
+    if (shade_batch < 1 || shade_batch > 64 || blocks_per_cu < 0 || blocks_per_cu > 8 || leaf_batch < 0 ||
+        leaf_batch > 64)
         return fail(GS_ERR_ARG, "bad tuning");
+    g_leaf_batch = leaf_batch;
     g_shade_batch = shade_batch;
     g_blocks_per_cu = blocks_per_cu;
     return GS_OK;
@@ -1138,6 +1155,7 @@ gs_status gs_render_tiles_debug_async(const gs_device_scene* ds, const gs_camera
     a.P = ds->params;
     a.root = ds->dev.root;
     a.shade_batch = g_shade_batch;
+    a.leaf_batch = g_leaf_batch;
     // Pageable source: the runtime stages it before returning, so `kp` may go out of scope.
     HIPCHK(hipMemcpyAsync(ds->params, &kp, sizeof(KParams), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(ds->queue, 0, 4, st));

@@ -29,8 +29,9 @@ def render(scene, seed=1):
     return out, cnt.as_dict()
 
 
-def set_tuning(shade_batch=32, blocks_per_cu=0):
-    N.check(N.lib.gs_set_tuning(shade_batch, blocks_per_cu))
+def set_tuning(shade_batch=60, blocks_per_cu=0, leaf_batch=0):
+    """Process-wide launch tuning (see gs_set_tuning in include/grayshift_gpu.h)."""
+    N.check(N.lib.gs_set_tuning(shade_batch, blocks_per_cu, leaf_batch))
 
 
 def write_ppm(path, rgb):

@@ -192,8 +192,9 @@ int32_t gs_version(void);
 
 /* Launch tuning, process-wide: shade_batch in [1, 64] = finished lanes a wave
  * collects before it shades them together; blocks_per_cu in [0, 8], 0 = from the
- * occupancy query. */
-gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu);
+ * occupancy query; leaf_batch in [0, 64] = lanes waiting at a leaf before the wave
+ * runs a leaf-test pass (0: leaves and nodes stepped in the same iteration). */
+gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf_batch);
 
 /* Upload a flattened scene to the current HIP device. */
 gs_status gs_device_scene_create(const gs_flat_scene* scene, gs_device_scene** out);
