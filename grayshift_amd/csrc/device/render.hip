@@ -439,6 +439,16 @@ __device__ GS_NOINLINE Scatter scatter(const DevScene& sc, HitRec h, d3 in_dir, 
 
 __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull << lane) - 1ull; }
 
+// Diagnostic build only (-DGS_STAMPS): per-wave shader-clock totals of the three loop
+// phases, written to their own debug buffer (the d_item_visits pointer, reinterpreted
+// as u64[3]) — never to an output.  The stamps' fences perturb scheduling, so only the
+// shares are meaningful, not the absolute time.
+#ifdef GS_STAMPS
+#define GS_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); t = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define GS_STAMP(t) do { } while (0)
+#endif
+
 // Per-lane pixel state lives in LDS ([field][lane], conflict-free), touched once per
 // path; the traversal stack follows it: [depth][lane] u32 refs.
 enum { L_CSR = 0, L_CSG, L_CSB, L_LSUM, L_LSQ, L_SCOUNT, L_ND };
@@ -527,7 +537,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     o[1] = (float)(LD(L_CSG) / scount);
                     o[2] = (float)(LD(L_CSB) / scount);
                     atomicAdd(&s_cnt[C_PIX], 1ull);
+#ifndef GS_STAMPS
                     if (P->item_visits) P->item_visits[item] = c_nodes;
+#endif
                     atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
                     atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
                     c_nodes = 0;
@@ -575,9 +587,11 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         }
     };
 
+    uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, acc_refill = 0, acc_trav = 0, acc_shade = 0;
 #pragma unroll 1
     for (;;) {
         // ---------------------------------------------------------- refill
+        GS_STAMP(ts0);
         uint64_t need = __ballot(st == S_NEED);
 #pragma unroll 1
         while (need != 0 && !qdone) {
@@ -634,6 +648,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         }
         if (st == S_NEED) st = S_DONE;
         if (__ballot(st == S_TRACE || st == S_SHADE) == 0) break;
+        GS_STAMP(ts1);
 
         // ------------------------------------------------------- traverse
 #pragma unroll 1
@@ -697,6 +712,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         }
 
         // ---------------------------------------------------------- shade
+        GS_STAMP(ts2);
         if (st == S_SHADE) {
             bool ends = true;
             double Lr = 0.0, Lg = 0.0, Lb = 0.0;
@@ -735,7 +751,21 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 advance();
             }
         }
+#ifdef GS_STAMPS
+        GS_STAMP(ts3);
+        acc_refill += ts1 - ts0;
+        acc_trav += ts2 - ts1;
+        acc_shade += ts3 - ts2;
+#endif
     }
+#ifdef GS_STAMPS
+    if (lane == 0 && P->item_visits) {
+        unsigned long long* dbg = (unsigned long long*)P->item_visits;
+        atomicAdd(&dbg[0], (unsigned long long)acc_refill);
+        atomicAdd(&dbg[1], (unsigned long long)acc_trav);
+        atomicAdd(&dbg[2], (unsigned long long)acc_shade);
+    }
+#endif
 #undef LD
 #undef LI
 

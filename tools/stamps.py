@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Phase split of the megakernel (diagnostic build variants/stamps.so, -DGS_STAMPS).
+GS_LIB=grayshift_amd/variants/stamps.so python tools/stamps.py [--config C4] [tuning]"""
+import argparse, ctypes as C, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C4")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--shade-batch", type=int, default=60)
+    ap.add_argument("--leaf-batch", type=int, default=0)
+    a = ap.parse_args()
+    import torch
+    import grayshift_amd as g
+    from grayshift_amd import _native as N, scenes
+    g.set_tuning(a.shade_batch, 0, a.leaf_batch)
+    sc = scenes.config(a.config, width=a.width, spp=a.spp)
+    r = g.Renderer(sc, 0, 1, 64)
+    dev = torch.device("cuda", 0)
+    packed = torch.zeros(r.capacity * 3, dtype=torch.float32, device=dev)
+    dbg = torch.zeros(max(4, r.capacity // 2 + 2), dtype=torch.int64, device=dev)
+    N.check(N.lib.gs_render_tiles_debug_async(r.dev, C.byref(r.cam), C.byref(r.settings), 1, C.byref(r.part),
+                                              C.c_void_p(packed.data_ptr()), None, C.c_void_p(dbg.data_ptr()), None))
+    torch.cuda.synchronize()
+    v = dbg[:3].cpu().tolist()
+    tot = sum(v)
+    print("refill %.1f%%  traverse %.1f%%  shade %.1f%%  (wave-clock totals %s)" % (
+        100 * v[0] / tot, 100 * v[1] / tot, 100 * v[2] / tot, v))
+
+
+if __name__ == "__main__":
+    main()
