@@ -75,7 +75,7 @@ def main():
     from grayshift_amd import scenes
 
     if a.shade_batch is not None or a.blocks_per_cu is not None or a.leaf_batch is not None:
-        g.set_tuning(a.shade_batch or 60, a.blocks_per_cu or 0, a.leaf_batch or 0)
+        g.set_tuning(a.shade_batch or 60, a.blocks_per_cu or 0, 8 if a.leaf_batch is None else a.leaf_batch)
     sc = scenes.config(a.config, width=a.width, spp=a.spp)
     r = g.Renderer(sc, rank=rank, world_size=world, tile=a.tile)
     # Every rank's packed buffer has rank 0's capacity (round-robin gives it the most tiles)

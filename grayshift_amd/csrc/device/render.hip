@@ -801,7 +801,7 @@ __global__ void gs_unpack_kernel(const float* __restrict__ in, float* __restrict
 static thread_local std::string tl_err;
 static int32_t g_shade_batch = 60;  // swept on MI355X C4: 32 -> 1459, 56 -> 1603, 60 -> 1623, 64 -> 1564 Msamples/s
 static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
-static int32_t g_leaf_batch = 0;
+static int32_t g_leaf_batch = 8;  // swept on MI355X C4: 0 -> 1940, 8 -> 1986, 16 -> 1923, 32 -> 1770 Msamples/s
 
 extern "C" void gs_set_last_error(const char* msg) { tl_err = msg ? msg : ""; }
 static gs_status fail(gs_status code, const std::string& msg) {
