@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--shade-batch", type=int, default=None)
     ap.add_argument("--blocks-per-cu", type=int, default=None)
     ap.add_argument("--leaf-batch", type=int, default=None)
+    ap.add_argument("--sample-chunk", type=int, default=None, help="samples per work item (-1 auto, 0 whole pixel)")
     ap.add_argument("--cpu-stride", type=int, default=4, help="CPU baseline: every Nth row and column")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
@@ -74,8 +75,8 @@ def main():
     import grayshift_amd as g
     from grayshift_amd import scenes
 
-    if a.shade_batch is not None or a.blocks_per_cu is not None or a.leaf_batch is not None:
-        g.set_tuning(a.shade_batch or 60, a.blocks_per_cu or 0, 8 if a.leaf_batch is None else a.leaf_batch)
+    g.set_tuning(a.shade_batch or 56, a.blocks_per_cu or 0, 8 if a.leaf_batch is None else a.leaf_batch,
+                 -1 if a.sample_chunk is None else a.sample_chunk)
     sc = scenes.config(a.config, width=a.width, spp=a.spp)
     r = g.Renderer(sc, rank=rank, world_size=world, tile=a.tile)
     # Every rank's packed buffer has rank 0's capacity (round-robin gives it the most tiles)

@@ -100,7 +100,7 @@ pub struct gs_counters {
 extern "C" {
     pub fn gs_last_error() -> *const c_char;
     pub fn gs_version() -> i32;
-    pub fn gs_set_tuning(shade_batch: i32, blocks_per_cu: i32, leaf_batch: i32) -> gs_status;
+    pub fn gs_set_tuning(shade_batch: i32, blocks_per_cu: i32, leaf_batch: i32, sample_chunk: i32) -> gs_status;
     pub fn gs_device_scene_create(scene: *const gs_flat_scene, out: *mut *mut gs_device_scene) -> gs_status;
     pub fn gs_device_scene_destroy(scene: *mut gs_device_scene) -> gs_status;
     pub fn gs_partition_capacity(cam: *const gs_camera, part: *const gs_partition) -> i64;

@@ -116,7 +116,7 @@ SIGNATURES = {
     # grayshift_gpu.h
     "gs_last_error": (C.c_char_p, []),
     "gs_version": (C.c_int32, []),
-    "gs_set_tuning": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32]),
+    "gs_set_tuning": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "gs_device_scene_create": (C.c_int32, [_P, C.POINTER(_P)]),
     "gs_device_scene_destroy": (C.c_int32, [_P]),
     "gs_partition_capacity": (C.c_int64, [C.POINTER(gs_camera), C.POINTER(gs_partition)]),

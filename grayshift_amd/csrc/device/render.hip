@@ -103,7 +103,13 @@ struct KParams {
     gs_sample_settings ss;
     uint64_t seed;
     int32_t rank, world_size, tile_w, tile_h, tiles_x, pad;
-    uint32_t capacity, pad2;
+    uint32_t capacity;  // packed pixel slots of this rank
+    // Sample chunking (single-batch settings only): work item q = (packed pixel q / cpp,
+    // samples [(q % cpp) * chunk, +chunk)); each item leaves its Σrgb in `partial` and
+    // gs_combine_kernel sums a pixel's chunks in chunk order.  chunk == 0: one item per
+    // pixel running the reference's batch loop (camera.rs:135-165) to completion.
+    uint32_t chunk, cpp, n_items, pad2;
+    double* partial;
     float* out;
     unsigned long long* counters;
     uint32_t* queue;
@@ -521,6 +527,22 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #pragma unroll 1
         for (;;) {
             if (LI(L_BLEFT) == 0) {
+                if (P->chunk) {  // end of a chunk: its Σrgb, summed per pixel by gs_combine_kernel
+                    const uint32_t item = LI(L_ITEM);
+                    double* o = P->partial + (size_t)item * 3;
+                    o[0] = LD(L_CSR);
+                    o[1] = LD(L_CSG);
+                    o[2] = LD(L_CSB);
+#ifndef GS_STAMPS
+                    if (P->item_visits) atomicAdd(&P->item_visits[item / P->cpp], c_nodes);
+#endif
+                    atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
+                    atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
+                    c_nodes = 0;
+                    c_sph = 0;
+                    st = S_NEED;
+                    return;
+                }
                 // end of a batch (camera.rs:149-164)
                 const double scount = LD(L_SCOUNT), lsum = LD(L_LSUM), lsq = LD(L_LSQ);
                 const double confidence_sq = P->ss.confidence * P->ss.confidence;
@@ -602,14 +624,17 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             base = __shfl(base, leader);
             const uint32_t tile_px = (uint32_t)(P->tile_w * P->tile_h);
             const bool blocked8 = (P->tile_w % 8 == 0) && (P->tile_h % 8 == 0);
-            if ((uint64_t)base + n >= (uint64_t)P->capacity) qdone = true;
+            if ((uint64_t)base + n >= (uint64_t)P->n_items) qdone = true;
             if (st == S_NEED) {
                 const uint64_t q = (uint64_t)base + (uint64_t)__popcll(need & lanemask_lt(lane));
-                if (q >= P->capacity) {
+                if (q >= P->n_items) {
                     st = S_DONE;
                 } else {
-                    // work order: 8x8 blocks inside each tile (coherent primary rays)
-                    const uint32_t slot = (uint32_t)(q / tile_px), w = (uint32_t)(q % tile_px);
+                    // work order: 8x8 blocks inside each tile (coherent primary rays), a
+                    // pixel's chunks adjacent
+                    const uint32_t cpp = P->cpp;
+                    const uint32_t pq = (uint32_t)(q / cpp), ck = (uint32_t)(q % cpp);
+                    const uint32_t slot = pq / tile_px, w = pq % tile_px;
                     uint32_t x, y;
                     if (blocked8) {
                         const uint32_t b = w >> 6, l = w & 63, bpr = (uint32_t)P->tile_w >> 3;
@@ -624,12 +649,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     const uint32_t pi = (tile % (uint32_t)P->tiles_x) * (uint32_t)P->tile_w + x;
                     const uint32_t pj = (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + y;
                     if (pi >= (uint32_t)cam.image_width || pj >= (uint32_t)cam.image_height) {
-                        float* o = P->out + (size_t)item * 3;  // padding pixel
-                        o[0] = 0.0f;
-                        o[1] = 0.0f;
-                        o[2] = 0.0f;
+                        if (!P->chunk) {  // padding pixel (chunked: gs_combine_kernel writes it)
+                            float* o = P->out + (size_t)item * 3;
+                            o[0] = 0.0f;
+                            o[1] = 0.0f;
+                            o[2] = 0.0f;
+                        }
                     } else {
-                        LI(L_ITEM) = item;
                         LI(L_PIX) = pj * (uint32_t)cam.image_width + pi;
                         LD(L_CSR) = 0.0;
                         LD(L_CSG) = 0.0;
@@ -638,8 +664,16 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         LD(L_LSQ) = 0.0;
                         // first batch starts (camera.rs:137)
                         LD(L_SCOUNT) = 0.0 + (double)P->ss.batch_size;
-                        LI(L_BLEFT) = P->ss.batch_size;
-                        sample = 0;
+                        if (P->chunk) {
+                            LI(L_ITEM) = item * cpp + ck;
+                            sample = ck * P->chunk;
+                            LI(L_BLEFT) = min(P->chunk, P->ss.batch_size - sample);
+                            if (ck == 0) atomicAdd(&s_cnt[C_PIX], 1ull);
+                        } else {
+                            LI(L_ITEM) = item;
+                            LI(L_BLEFT) = P->ss.batch_size;
+                            sample = 0;
+                        }
                         advance();
                     }
                 }
@@ -776,6 +810,37 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     if (threadIdx.x < C_N && P->counters) atomicAdd(&P->counters[threadIdx.x], s_cnt[threadIdx.x]);
 }
 
+// Chunked single-batch renders: a pixel's colour is the sum of its chunks' Σrgb, taken
+// in chunk (= sample) order, over the batch size (camera.rs:142-160 with one batch).
+// Padding slots of partial tiles get zeros.
+__global__ void gs_combine_kernel(const KParams* __restrict__ P) {
+    const uint32_t tile_px = (uint32_t)(P->tile_w * P->tile_h), cpp = P->cpp;
+    const double scount = 0.0 + (double)P->ss.batch_size;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < P->capacity; k += gridDim.x * blockDim.x) {
+        const uint32_t slot = k / tile_px, w = k % tile_px;
+        const uint32_t tile = (uint32_t)P->rank + slot * (uint32_t)P->world_size;
+        const uint32_t pi = (tile % (uint32_t)P->tiles_x) * (uint32_t)P->tile_w + w % (uint32_t)P->tile_w;
+        const uint32_t pj = (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + w / (uint32_t)P->tile_w;
+        float* o = P->out + (size_t)k * 3;
+        if (pi >= (uint32_t)P->cam.image_width || pj >= (uint32_t)P->cam.image_height) {
+            o[0] = 0.0f;
+            o[1] = 0.0f;
+            o[2] = 0.0f;
+            continue;
+        }
+        const double* p = P->partial + (size_t)k * cpp * 3;
+        double r = 0.0, g = 0.0, b = 0.0;
+        for (uint32_t c = 0; c < cpp; c++) {
+            r += p[c * 3];
+            g += p[c * 3 + 1];
+            b += p[c * 3 + 2];
+        }
+        o[0] = (float)(r / scount);
+        o[1] = (float)(g / scount);
+        o[2] = (float)(b / scount);
+    }
+}
+
 // Scatter rank-packed tiles into the frame.
 __global__ void gs_unpack_kernel(const float* __restrict__ in, float* __restrict__ frame, int32_t W, int32_t H,
                                  int32_t world, int32_t tile_w, int32_t tile_h, int32_t tiles_x, uint64_t capacity) {
@@ -799,9 +864,10 @@ __global__ void gs_unpack_kernel(const float* __restrict__ in, float* __restrict
 
 // =============================================================== host side
 static thread_local std::string tl_err;
-static int32_t g_shade_batch = 60;  // swept on MI355X C4: 32 -> 1459, 56 -> 1603, 60 -> 1623, 64 -> 1564 Msamples/s
+static int32_t g_shade_batch = 56;  // swept on MI355X C4 (chunked): 48 -> 3390, 52 -> 3422, 56 -> 3428, 60 -> 3190 Msamples/s
 static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
-static int32_t g_leaf_batch = 8;  // swept on MI355X C4: 0 -> 1940, 8 -> 1986, 16 -> 1923, 32 -> 1770 Msamples/s
+static int32_t g_leaf_batch = 8;
+static int32_t g_sample_chunk = -1;  // -1 auto, 0 never split a pixel's samples  // swept on MI355X C4: 0 -> 1940, 8 -> 1986, 16 -> 1923, 32 -> 1770 Msamples/s
 
 extern "C" void gs_set_last_error(const char* msg) { tl_err = msg ? msg : ""; }
 static gs_status fail(gs_status code, const std::string& msg) {
@@ -823,6 +889,8 @@ struct gs_device_scene {
     DevScene dev{};
     uint32_t n_nodes = 0;
     uint32_t stack_depth = 1;  // LDS stack entries per lane (= BVH depth)
+    double* partial = nullptr;  // chunk partial sums, grown on demand
+    size_t partial_bytes = 0;
 };
 
 namespace {
@@ -988,10 +1056,11 @@ extern "C" {
 const char* gs_last_error(void) { return tl_err.c_str(); }
 int32_t gs_version(void) { return GS_ABI_VERSION; }
 
-gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf_batch) {
+gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf_batch, int32_t sample_chunk) {
     if (shade_batch < 1 || shade_batch > 64 || blocks_per_cu < 0 || blocks_per_cu > 8 || leaf_batch < 0 ||
-        leaf_batch > 64)
+        leaf_batch > 64 || sample_chunk < -1)
         return fail(GS_ERR_ARG, "bad tuning");
+    g_sample_chunk = sample_chunk;
     g_leaf_batch = leaf_batch;
     g_shade_batch = shade_batch;
     g_blocks_per_cu = blocks_per_cu;
@@ -1125,6 +1194,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
 gs_status gs_device_scene_destroy(gs_device_scene* ds) {
     if (!ds) return GS_OK;
     if (ds->mem) (void)hipFree(ds->mem);
+    if (ds->partial) (void)hipFree(ds->partial);
     delete ds;
     return GS_OK;
 }
@@ -1175,6 +1245,35 @@ gs_status gs_render_tiles_debug_async(const gs_device_scene* ds, const gs_camera
     kp.tile_h = part->tile_h;
     kp.tiles_x = (cam->image_width + part->tile_w - 1) / part->tile_w;
     kp.capacity = (uint32_t)cap;
+    // Split pixels into sample chunks only when the settings run exactly one batch:
+    // max_samples < batch_size makes the first stop test (camera.rs:158) always true.
+    uint32_t chunk = 0, cpp = 1;
+    if (g_sample_chunk != 0 && ss->max_samples < ss->batch_size) {
+        const uint32_t bs = ss->batch_size;
+        uint32_t c = g_sample_chunk > 0 ? (uint32_t)g_sample_chunk : std::max<uint32_t>(32u, (bs + 31u) / 32u);
+        if ((bs + c - 1) / c > 64u) c = (bs + 63u) / 64u;  // at most 64 chunks per pixel
+        if (c < bs) {
+            chunk = c;
+            cpp = (bs + c - 1) / c;
+        }
+    }
+    if ((uint64_t)cap * cpp >= 0xFFFFFFFFull) chunk = 0, cpp = 1;
+    kp.chunk = chunk;
+    kp.cpp = cpp;
+    kp.n_items = (uint32_t)cap * cpp;
+    if (chunk) {
+        const size_t need = (size_t)kp.n_items * 3 * sizeof(double);
+        gs_device_scene* mds = const_cast<gs_device_scene*>(ds);
+        if (mds->partial_bytes < need) {
+            if (mds->partial) (void)hipFree(mds->partial);  // synchronises: no launch still reads it
+            mds->partial = nullptr;
+            mds->partial_bytes = 0;
+            if (hipMalloc(&mds->partial, need) != hipSuccess)
+                return fail(GS_ERR_OOM, "hipMalloc of " + std::to_string(need) + " bytes of chunk sums failed");
+            mds->partial_bytes = need;
+        }
+        kp.partial = mds->partial;
+    }
     kp.out = d_out;
     kp.counters = (unsigned long long*)d_counters;
     kp.queue = ds->queue;
@@ -1199,12 +1298,17 @@ gs_status gs_render_tiles_debug_async(const gs_device_scene* ds, const gs_camera
         per_cu = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
     }
     int64_t blocks = (int64_t)cus * per_cu;
-    // no more waves than work: one lane per pixel at most
-    int64_t max_blocks = (cap + GS_BLOCK - 1) / GS_BLOCK;
+    // no more waves than work: one lane per item at most
+    int64_t max_blocks = ((int64_t)kp.n_items + GS_BLOCK - 1) / GS_BLOCK;
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(gs_render_kernel, dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
+    if (chunk) {
+        const unsigned grid = (unsigned)std::min<int64_t>((cap + 255) / 256, 8192);
+        hipLaunchKernelGGL(gs_combine_kernel, dim3(grid), dim3(256), 0, st, (const KParams*)ds->params);
+        HIPCHK(hipGetLastError());
+    }
     return GS_OK;
 }
 

@@ -193,8 +193,13 @@ int32_t gs_version(void);
 /* Launch tuning, process-wide: shade_batch in [1, 64] = finished lanes a wave
  * collects before it shades them together; blocks_per_cu in [0, 8], 0 = from the
  * occupancy query; leaf_batch in [0, 64] = lanes waiting at a leaf before the wave
- * runs a leaf-test pass (0: leaves and nodes stepped in the same iteration). */
-gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf_batch);
+ * runs a leaf-test pass (0: leaves and nodes stepped in the same iteration);
+ * sample_chunk = samples per work item when the settings run a single batch
+ * (max_samples < batch_size, as every fixed-spp render): -1 auto (32, or batch/32 for
+ * big batches, at most 64 chunks per pixel), 0 never split a pixel, n > 0 explicit.
+ * Chunks keep every sample's RNG stream; a pixel's chunk sums are added in sample order,
+ * so only the association of the f64 colour sum differs from the sequential loop. */
+gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf_batch, int32_t sample_chunk);
 
 /* Upload a flattened scene to the current HIP device. */
 gs_status gs_device_scene_create(const gs_flat_scene* scene, gs_device_scene** out);

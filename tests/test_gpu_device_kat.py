@@ -35,7 +35,7 @@ def _rays(rng, n, special=True):
     d = rng.normal(size=(n, 3))
     if special:
         k = n // 4
-        d[:k, rng.integers(0, 3, k)] = 0.0                       # axis-parallel rays (1/0 = inf)
+        d[np.arange(k), rng.integers(0, 3, k)] = 0.0             # axis-parallel rays (1/0 = inf)
         d[k:2 * k, 0] = -0.0                                     # negative zero component
         o[2 * k:3 * k, 1] = np.round(o[2 * k:3 * k, 1])          # origins on integer planes
     return np.ascontiguousarray(np.hstack([o, d]))
@@ -46,7 +46,15 @@ def test_aabb_matches_oracle(kat):
     n = 20000
     ray = _rays(rng, n)
     lo = np.floor(rng.uniform(-3, 2, (n, 3)))
-    box = np.ascontiguousarray(np.hstack([lo, lo + np.floor(rng.uniform(0, 3, (n, 3)))]))  # some flat boxes
+    ext = 1.0 + np.floor(rng.uniform(0, 3, (n, 3)))
+    ext[rng.random(n) < 0.05, rng.integers(0, 3)] = 0.0                 # a few flat boxes
+    box = np.ascontiguousarray(np.hstack([lo, lo + ext]))
+    # aim 60% of the rays near their box (keeping the zero / negative-zero components) so
+    # hits and misses are both common
+    aim = rng.random(n) < 0.6
+    to_box = 0.5 * (box[:, :3] + box[:, 3:]) - ray[:, :3] + rng.normal(scale=0.4, size=(n, 3))
+    d = ray[:, 3:]
+    ray[:, 3:] = np.where(aim[:, None] & (d != 0), to_box, d)
     iv = np.ascontiguousarray(np.stack([np.full(n, 0.001), np.where(rng.random(n) < 0.5, 1e300,
                                                                       rng.uniform(0, 6, n))], 1))
     out = np.zeros(n, np.int32)
@@ -81,6 +89,9 @@ def test_triangle_matches_oracle_bitwise(kat):
     n = 20000
     ray = _rays(rng, n, special=False)
     tri = np.ascontiguousarray(rng.uniform(-2, 2, (n, 9)))
+    aim = rng.random(n) < 0.6  # towards the centroid, so hits are common
+    cen = (tri[:, 0:3] + tri[:, 3:6] + tri[:, 6:9]) / 3.0
+    ray[aim, 3:] = cen[aim] - ray[aim, :3] + rng.normal(scale=0.3, size=(int(aim.sum()), 3))
     tuv = np.zeros((n, 3))
     hit = np.zeros(n, np.int32)
     assert kat.kat_tri(n, ptr(tri), ptr(ray), ptr(tuv), ptr(hit)) == 0

@@ -178,6 +178,61 @@ def test_partition_invariance(world, tile):
     assert fc == pc
 
 
+# ------------------------------------------------------ sample chunking
+class _chunk:
+    """Force gs_set_tuning's sample_chunk for one render (restores auto)."""
+    def __init__(self, n):
+        self.n = n
+
+    def __enter__(self):
+        g.set_tuning(56, 0, 8, self.n)
+
+    def __exit__(self, *a):
+        g.set_tuning(56, 0, 8, -1)
+
+
+@pytest.mark.parametrize("name", ["C4", "C3", "earth_fixed"])
+@pytest.mark.parametrize("chunk", [1, 3, 5, 16, 0])
+def test_sample_chunks_match_oracle(name, chunk):
+    """Single-batch renders split into sample chunks (one work item each): every
+    sample keeps its RNG stream, so counters are the oracle's and the colour differs
+    only by the association of the f64 sum (tolerance as everywhere)."""
+    if name == "earth_fixed":
+        base = scenes.SCENES["earth"](width=48)
+        sc = scenes.Scene("earth16", base.spec, base.camera, fixed_spp(16))
+    else:
+        sc = scenes.config(name, width=64, spp=16)
+    with _chunk(chunk):
+        out, gc = g.render(sc, seed=13)
+    ref, rc = oracle.render(sc, seed=13)
+    assert maxdiff(out, ref) < TOL and counters_match(gc, rc)
+    with _chunk(0):
+        whole, wc = g.render(sc, seed=13)
+    assert wc == gc
+    # same samples, re-associated sum: a few f32 ulps at most, mostly identical
+    assert np.allclose(out, whole, rtol=4e-7, atol=1e-30)
+    assert (out == whole).mean() > 0.98
+
+
+def test_chunking_ignored_for_multi_batch_settings():
+    sc = _custom(20, 1.0, batch=3, maxs=17, tol=0.1)
+    with _chunk(1):
+        a, ca = g.render(sc, seed=5)
+    with _chunk(0):
+        b, cb = g.render(sc, seed=5)
+    assert np.array_equal(a, b) and ca == cb
+
+
+@pytest.mark.parametrize("world,tile,chunk", [(3, 16, 3), (8, 8, 1), (2, 64, 7)])
+def test_partition_invariance_chunked(world, tile, chunk):
+    sc = scenes.config("C5", width=80, spp=8)
+    with _chunk(chunk):
+        full, fc = g.render(sc, seed=3)
+        part, pc = _render_partitioned(sc, world, tile, seed=3)
+    assert np.array_equal(full, part)
+    assert fc == pc
+
+
 # ----------------------------------------------- BASELINE-size properties
 def _spot_check(sc, out, seed, n=96):
     rng = np.random.default_rng(123)

@@ -40,9 +40,11 @@ def test_every_declared_symbol_is_exported(built):
 
 def test_version_and_error_channel():
     assert N.lib.gs_version() == 1
-    assert N.lib.gs_set_tuning(0, 0, 0) == N.GS_ERR_ARG
+    assert N.lib.gs_set_tuning(0, 0, 0, -1) == N.GS_ERR_ARG
     assert b"tuning" in N.lib.gs_last_error()
-    assert N.lib.gs_set_tuning(60, 0, 0) == N.GS_OK
+    assert N.lib.gs_set_tuning(60, 0, 0, -1) == N.GS_OK
+    assert N.lib.gs_set_tuning(60, 0, 8, -2) == N.GS_ERR_ARG
+    assert N.lib.gs_set_tuning(60, 0, 8, -1) == N.GS_OK
 
 
 @pytest.mark.parametrize("name", ["gs_object", "gs_material_spec", "gs_texture_spec", "gs_image_spec",

@@ -12,12 +12,13 @@ def main():
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--shade-batch", type=int, default=60)
-    ap.add_argument("--leaf-batch", type=int, default=0)
+    ap.add_argument("--leaf-batch", type=int, default=8)
+    ap.add_argument("--sample-chunk", type=int, default=-1)
     a = ap.parse_args()
     import torch
     import grayshift_amd as g
     from grayshift_amd import _native as N, scenes
-    g.set_tuning(a.shade_batch, 0, a.leaf_batch)
+    g.set_tuning(a.shade_batch, 0, a.leaf_batch, a.sample_chunk)
     sc = scenes.config(a.config, width=a.width, spp=a.spp)
     r = g.Renderer(sc, 0, 1, 64)
     dev = torch.device("cuda", 0)
