@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--blocks-per-cu", type=int, default=None)
     ap.add_argument("--leaf-batch", type=int, default=None)
     ap.add_argument("--sample-chunk", type=int, default=None, help="samples per work item (-1 auto, 0 whole pixel)")
-    ap.add_argument("--cpu-stride", type=int, default=4, help="CPU baseline: every Nth row and column")
+    ap.add_argument("--cpu-stride", type=int, default=3, help="CPU baseline: every Nth row and column")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_C4_latest.json"),

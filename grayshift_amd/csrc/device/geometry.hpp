@@ -59,6 +59,29 @@ __device__ __forceinline__ bool box_hit(const DNode& n, const d3& o, const d3& i
     return !(hi <= lo);
 }
 
+// Rays whose slab times can never be NaN — every 1/d finite and non-zero, |origin| and
+// every box coordinate below 1e300 (so mn - o is finite; finite x finite non-zero is
+// never NaN) — take the swap as (min, max): for non-NaN t0 != t1 that is exactly the
+// compare-select; for t0 == t1 the two are the same value up to the sign of zero, and
+// lo / hi only ever meet comparisons, where ±0 are equal.  3 x (cmp + 4 cndmask) -> 3 x 2.
+__device__ __forceinline__ bool fast_slab_ray(const d3& o, const d3& inv) {
+    auto ok = [](double v) { return __builtin_fabs(v) <= 1.7976931348623157e308 && v != 0.0; };
+    auto small = [](double v) { return __builtin_fabs(v) < 1e300; };
+    return ok(inv.x) && ok(inv.y) && ok(inv.z) && small(o.x) && small(o.y) && small(o.z);
+}
+__device__ __forceinline__ void slab_fast(double mn, double mx, double o, double inv, double& lo, double& hi) {
+    const double t0 = (mn - o) * inv, t1 = (mx - o) * inv;
+    lo = fmax(lo, fmin(t0, t1));
+    hi = fmin(hi, fmax(t0, t1));
+}
+__device__ __forceinline__ bool box_hit_fast(const DNode& n, const d3& o, const d3& inv, double tmin, double tmax) {
+    double lo = tmin, hi = tmax;
+    slab_fast(n.mnx, n.mxx, o.x, inv.x, lo, hi);
+    slab_fast(n.mny, n.mxy, o.y, inv.y, lo, hi);
+    slab_fast(n.mnz, n.mxz, o.z, inv.z, lo, hi);
+    return !(hi <= lo);
+}
+
 // Sphere::hit acceptance (sphere.rs:64-88): returns t or a NaN-free miss flag.
 __device__ __forceinline__ bool sphere_accept(d3 c, double r, const Ray& ray, double a, double tmin, double tmax,
                                          double& t_out) {

@@ -123,10 +123,23 @@ struct KArgs {
     const KParams* P;
     uint32_t root;
     int32_t shade_batch;
-    int32_t leaf_batch;  // 0: test leaves in the same iteration as node steps (if-if)
+    int32_t leaf_batch;  // >= 1: tracing lanes at a leaf before a wave runs a leaf pass
+    int32_t fast_boxes;  // every node coordinate |x| < 1e300: rays may take box_hit_fast
 };
 
 enum { S_NEED = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };
+
+// Device-side refs in node children / the root / the traversal stack: a BVH node is its
+// bare index (< 2^26), leaves keep their ABI tag (kind >= 2 in the top 4 bits), and
+// "none" is all ones.  So `cur >= DREF_LEAF` tells a leaf in one compare and a node's
+// byte offset is `cur << 6`.  (Leaf, list and instance records keep ABI refs.)
+#define DREF_NONE 0xFFFFFFFFu
+#define DREF_LEAF (1u << GS_REF_SHIFT)
+__host__ __device__ inline uint32_t device_ref(uint32_t abi_ref) {
+    if (abi_ref == GS_REF_NONE) return DREF_NONE;
+    if ((abi_ref >> GS_REF_SHIFT) == GS_REF_NODE) return abi_ref & GS_REF_MASK;
+    return abi_ref;
+}
 
 // Outcome of testing one non-node child against the ray.
 struct LeafHit {
@@ -461,7 +474,7 @@ enum { L_CSR = 0, L_CSG, L_CSB, L_LSUM, L_LSQ, L_SCOUNT, L_ND };
 enum { L_ITEM = 0, L_PIX, L_BLEFT, L_NI };
 
 __host__ __device__ inline size_t lds_bytes(uint32_t stack_depth) {
-    return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4 + stack_depth * 4);
+    return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4 + (stack_depth + 1) * 4);  // + the dummy slot 0
 }
 
 __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs A) {
@@ -494,14 +507,18 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     ray.time = 0;
     d3 inv = mk(0, 0, 0);
     // traversal state
-    uint32_t cur = GS_REF_NONE, sp = 0, hit_ref = GS_REF_NONE, hit_inst = GS_REF_NONE;
+    uint32_t cur = DREF_NONE, sp = 0, hit_ref = GS_REF_NONE, hit_inst = GS_REF_NONE;
     double closest = 0.0;
+    bool fast = false;  // this ray's slab times can never be NaN (geometry.hpp box_hit_fast)
     // hot counters kept in registers, flushed per pixel
     uint32_t c_nodes = 0, c_sph = 0;
 
     auto begin_ray = [&]() {
         inv = mk(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
-        cur = A.root;
+#ifndef GS_NO_FAST_SLAB
+        fast = A.fast_boxes && fast_slab_ray(ray.o, inv);
+#endif
+        cur = A.root;  // a device ref (DREF_*)
         sp = 0;
         closest = 1.7976931348623157e308;  // f64::MAX (camera.rs:177)
         hit_ref = GS_REF_NONE;
@@ -610,11 +627,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     };
 
     uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, acc_refill = 0, acc_trav = 0, acc_shade = 0;
+    uint64_t it_all = 0, it_node = 0, it_leaf = 0, ln_node = 0, ln_leaf = 0, it_shade = 0, ln_shade = 0;
 #pragma unroll 1
     for (;;) {
         // ---------------------------------------------------------- refill
         GS_STAMP(ts0);
-        uint64_t need = __ballot(st == S_NEED);
+        uint64_t need = __builtin_amdgcn_ballot_w64(st == S_NEED);
 #pragma unroll 1
         while (need != 0 && !qdone) {
             const uint32_t n = (uint32_t)__popcll(need);
@@ -678,75 +696,95 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                 }
             }
-            need = __ballot(st == S_NEED);
+            need = __builtin_amdgcn_ballot_w64(st == S_NEED);
         }
         if (st == S_NEED) st = S_DONE;
-        if (__ballot(st == S_TRACE || st == S_SHADE) == 0) break;
+        if (__builtin_amdgcn_ballot_w64(st == S_TRACE || st == S_SHADE) == 0) break;
         GS_STAMP(ts1);
 
         // ------------------------------------------------------- traverse
+        // Within this phase a lane is TRACE, SHADE or DONE and rays do not change, so the
+        // shade count and the slab flavour are wave-uniform SGPR facts: no per-iteration
+        // ballot for the former, a scalar branch (no exec-mask juggling) for the latter.
+        const uint64_t alive = __builtin_amdgcn_ballot_w64(st != S_DONE);
+        const bool wave_fast = __builtin_amdgcn_ballot_w64(st == S_TRACE && !fast) == 0;
 #pragma unroll 1
         for (;;) {
-            const uint64_t tr = __ballot(st == S_TRACE);
+            const bool tracing = st == S_TRACE;
+            const uint64_t tr = __builtin_amdgcn_ballot_w64(tracing);
             if (tr == 0) break;
-            if ((uint32_t)__popcll(__ballot(st == S_SHADE)) >= (uint32_t)A.shade_batch) break;
+            if ((uint32_t)__popcll(alive & ~tr) >= (uint32_t)A.shade_batch) break;
             // Leaf batching: step nodes until `leaf_batch` tracing lanes sit at a leaf (or all
             // do), then test those leaves together, so a wave pays for the node step and the
             // sphere test in different iterations instead of both in every one.  Each lane
-            // still processes its refs in the reference's order.
-            const bool tracing = st == S_TRACE;
-            const bool at_leaf = tracing && (cur >> GS_REF_SHIFT) != GS_REF_NODE;
-            bool leaf_pass;
-            if (A.leaf_batch == 0) {
-                leaf_pass = at_leaf;  // if-if: both kinds every iteration
-            } else {
-                const uint64_t lm = __ballot(at_leaf);
-                leaf_pass = lm == tr || (uint32_t)__popcll(lm) >= (uint32_t)A.leaf_batch;
-            }
-            if (tracing) {
-                if (!at_leaf && (A.leaf_batch == 0 || !leaf_pass)) {
+            // still processes its refs in the reference's order.  The pass kind is uniform.
+            const bool at_leaf = tracing && cur >= DREF_LEAF;
+            const uint64_t lm = tr & __builtin_amdgcn_ballot_w64(cur >= DREF_LEAF);  // == ballot(at_leaf)
+            const bool leaf_pass = lm == tr || (uint32_t)__popcll(lm) >= (uint32_t)A.leaf_batch;
+#ifdef GS_STAMPS
+            it_all++;
+            it_node += !leaf_pass;
+            it_leaf += leaf_pass;
+            ln_node += leaf_pass ? 0ull : (uint64_t)__popcll(tr & ~lm);
+            ln_leaf += leaf_pass ? (uint64_t)__popcll(lm) : 0ull;
+#endif
+            if (!leaf_pass) {
+                if (tracing && !at_leaf) {
                     // All 64 B in one go (4 x dwordx4) and a branchless push: the child refs
                     // are always consumed, so the compiler cannot defer their load behind
-                    // the box test (which cost a second dependent memory round trip).
-                    const DNode nd = load_node(A.nodes + (cur & GS_REF_MASK));
+                    // the box test (a second dependent memory round trip).  Device node refs
+                    // are bare indices: byte offset = cur << 6, one VALU op off the SGPR base.
+                    const DNode nd = load_node((const DNode*)((const char*)A.nodes + (cur << 6)));
                     c_nodes++;
-                    const bool h = box_hit(nd, ray.o, inv, tmin, closest);
-                    s_stack[sp * GS_BLOCK + tid] = nd.right;  // in bounds: sp < BVH depth here
-                    sp += (h && nd.right != GS_REF_NONE) ? 1u : 0u;
-                    cur = h ? nd.left : (uint32_t)GS_REF_NONE;
-                } else if (at_leaf && leaf_pass) {
-                    if ((cur >> GS_REF_SHIFT) == GS_REF_SPHERE) {
-                        c_sph++;
-                        const DSphere s = A.spheres[cur & GS_REF_MASK];
-                        double t;
-                        if (sphere_accept(mk(s.cx, s.cy, s.cz), s.r, ray, len2(ray.d), tmin, closest, t)) {
-                            closest = t;
-                            hit_ref = cur;
-                            hit_inst = GS_REF_NONE;
-                        }
+                    bool h;
+                    if (wave_fast) {
+                        h = box_hit_fast(nd, ray.o, inv, tmin, closest);
                     } else {
-                        const LeafHit lh = leaf_other(sc, cur, ray, tmin, closest, s_cnt);
-                        if (lh.hit) {
-                            closest = lh.t;
-                            hit_ref = lh.ref;
-                            hit_inst = lh.inst;
-                        }
+                        h = box_hit(nd, ray.o, inv, tmin, closest);
                     }
-                    cur = GS_REF_NONE;
+                    s_stack[(sp + 1u) * GS_BLOCK + tid] = nd.right;  // slot sp+1 <= BVH depth
+                    sp += (h && nd.right != DREF_NONE) ? 1u : 0u;
+                    cur = h ? nd.left : DREF_NONE;
                 }
-                if (cur == GS_REF_NONE) {
-                    if (sp > 0) {
-                        sp--;
-                        cur = s_stack[sp * GS_BLOCK + tid];
-                    } else {
-                        st = S_SHADE;
+            } else if (at_leaf) {
+                if ((cur >> GS_REF_SHIFT) == GS_REF_SPHERE) {
+                    c_sph++;
+                    const DSphere s = *(const DSphere*)((const char*)A.spheres + (cur << 5));
+                    double t;
+                    if (sphere_accept(mk(s.cx, s.cy, s.cz), s.r, ray, len2(ray.d), tmin, closest, t)) {
+                        closest = t;
+                        hit_ref = cur;
+                        hit_inst = GS_REF_NONE;
+                    }
+                } else {
+                    const LeafHit lh = leaf_other(sc, cur, ray, tmin, closest, s_cnt);
+                    if (lh.hit) {
+                        closest = lh.t;
+                        hit_ref = lh.ref;
+                        hit_inst = lh.inst;
                     }
                 }
+                cur = DREF_NONE;
             }
+            // Branchless pop.  Entry k of the stack lives in slot k + 1 and slot 0 is a
+            // dummy, so the read below is in bounds for every sp in [0, depth].
+            const bool empty = tracing && cur == DREF_NONE;
+            const bool pop = empty && sp != 0;
+            const uint32_t top = s_stack[sp * GS_BLOCK + tid];
+            cur = pop ? top : cur;
+            sp -= pop ? 1u : 0u;
+            st = (empty && !pop) ? (uint32_t)S_SHADE : st;
         }
 
         // ---------------------------------------------------------- shade
         GS_STAMP(ts2);
+#ifdef GS_STAMPS
+        {
+            const uint64_t sm = __builtin_amdgcn_ballot_w64(st == S_SHADE);
+            it_shade += sm != 0;
+            ln_shade += (uint64_t)__popcll(sm);
+        }
+#endif
         if (st == S_SHADE) {
             bool ends = true;
             double Lr = 0.0, Lg = 0.0, Lb = 0.0;
@@ -798,6 +836,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         atomicAdd(&dbg[0], (unsigned long long)acc_refill);
         atomicAdd(&dbg[1], (unsigned long long)acc_trav);
         atomicAdd(&dbg[2], (unsigned long long)acc_shade);
+        atomicAdd(&dbg[3], (unsigned long long)it_all);
+        atomicAdd(&dbg[4], (unsigned long long)it_node);
+        atomicAdd(&dbg[5], (unsigned long long)it_leaf);
+        atomicAdd(&dbg[6], (unsigned long long)ln_node);
+        atomicAdd(&dbg[7], (unsigned long long)ln_leaf);
+        atomicAdd(&dbg[8], (unsigned long long)it_shade);
+        atomicAdd(&dbg[9], (unsigned long long)ln_shade);
     }
 #endif
 #undef LD
@@ -889,6 +934,7 @@ struct gs_device_scene {
     DevScene dev{};
     uint32_t n_nodes = 0;
     uint32_t stack_depth = 1;  // LDS stack entries per lane (= BVH depth)
+    bool fast_boxes = false;  // every node coordinate |x| < 1e300
     double* partial = nullptr;  // chunk partial sums, grown on demand
     size_t partial_bytes = 0;
 };
@@ -911,6 +957,8 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out) {
     auto bad = [](const std::string& m) { return fail(GS_ERR_ARG, "invalid flat scene: " + m); };
     auto unsup = [](const std::string& m) { return fail(GS_ERR_UNSUPPORTED, m); };
     if (!s.nodes && s.n_nodes) return bad("nodes");
+    // the kernel forms node / sphere byte offsets as u32 (ref << 6, ref << 5)
+    if (s.n_nodes >= (1u << 26) || s.n_spheres >= (1u << 27)) return unsup("more than 2^26 BVH nodes or 2^27 spheres");
     if (s.n_materials == 0 || !s.materials) return bad("no materials");
     auto prim_ok = [&](uint32_t r) {
         uint32_t k = r >> GS_REF_SHIFT, i = r & GS_REF_MASK;
@@ -1079,7 +1127,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     std::vector<DNode> nodes(s->n_nodes);
     for (uint32_t i = 0; i < s->n_nodes; i++) {
         const gs_node& n = s->nodes[i];
-        nodes[i] = DNode{n.min[0], n.min[1], n.min[2], n.max[0], n.max[1], n.max[2], n.left, n.right, 0, 0};
+        nodes[i] = DNode{n.min[0], n.min[1], n.min[2], n.max[0], n.max[1], n.max[2],
+                         device_ref(n.left), device_ref(n.right), 0, 0};
     }
     std::vector<DSphere> sph(s->n_spheres);
     std::vector<uint32_t> sph_mat(s->n_spheres);
@@ -1182,11 +1231,15 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     d.hdri = (const float*)(b + o_hdri);
     d.hdri_rgbe = rgbe.empty() ? nullptr : (const uint32_t*)(b + o_rgbe);
     d.bg = s->background;
-    d.root = s->root;
+    d.root = device_ref(s->root);
     ds->queue = (uint32_t*)(b + o_queue);
     ds->params = (KParams*)(b + o_params);
     ds->n_nodes = s->n_nodes;
     ds->stack_depth = depth < 1 ? 1 : depth;
+    ds->fast_boxes = true;
+    for (uint32_t i = 0; i < s->n_nodes && ds->fast_boxes; i++)
+        for (int k = 0; k < 3; k++)
+            if (!(std::fabs(s->nodes[i].min[k]) < 1e300 && std::fabs(s->nodes[i].max[k]) < 1e300)) ds->fast_boxes = false;
     *out = ds;
     return GS_OK;
 }
@@ -1283,8 +1336,9 @@ gs_status gs_render_tiles_debug_async(const gs_device_scene* ds, const gs_camera
     a.spheres = ds->dev.spheres;
     a.P = ds->params;
     a.root = ds->dev.root;
+    a.fast_boxes = ds->fast_boxes ? 1 : 0;
     a.shade_batch = g_shade_batch;
-    a.leaf_batch = g_leaf_batch;
+    a.leaf_batch = g_leaf_batch < 1 ? 1 : g_leaf_batch;  // 0 would never step a node
     // Pageable source: the runtime stages it before returning, so `kp` may go out of scope.
     HIPCHK(hipMemcpyAsync(ds->params, &kp, sizeof(KParams), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(ds->queue, 0, 4, st));

@@ -193,7 +193,7 @@ int32_t gs_version(void);
 /* Launch tuning, process-wide: shade_batch in [1, 64] = finished lanes a wave
  * collects before it shades them together; blocks_per_cu in [0, 8], 0 = from the
  * occupancy query; leaf_batch in [0, 64] = lanes waiting at a leaf before the wave
- * runs a leaf-test pass (0: leaves and nodes stepped in the same iteration);
+ * runs a leaf-test pass (0 acts as 1);
  * sample_chunk = samples per work item when the settings run a single batch
  * (max_samples < batch_size, as every fixed-spp render): -1 auto (32, or batch/32 for
  * big batches, at most 64 chunks per pixel), 0 never split a pixel, n > 0 explicit.

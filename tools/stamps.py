@@ -23,7 +23,7 @@ def main():
     r = g.Renderer(sc, 0, 1, 64)
     dev = torch.device("cuda", 0)
     packed = torch.zeros(r.capacity * 3, dtype=torch.float32, device=dev)
-    dbg = torch.zeros(max(4, r.capacity // 2 + 2), dtype=torch.int64, device=dev)
+    dbg = torch.zeros(max(16, r.capacity // 2 + 2), dtype=torch.int64, device=dev)
     N.check(N.lib.gs_render_tiles_debug_async(r.dev, C.byref(r.cam), C.byref(r.settings), 1, C.byref(r.part),
                                               C.c_void_p(packed.data_ptr()), None, C.c_void_p(dbg.data_ptr()), None))
     torch.cuda.synchronize()
@@ -31,6 +31,10 @@ def main():
     tot = sum(v)
     print("refill %.1f%%  traverse %.1f%%  shade %.1f%%  (wave-clock totals %s)" % (
         100 * v[0] / tot, 100 * v[1] / tot, 100 * v[2] / tot, v))
+    it_all, it_node, it_leaf, ln_node, ln_leaf, it_shade, ln_shade = dbg[3:10].cpu().tolist()
+    print("traversal iterations %d: node passes %d (%.1f active lanes), leaf passes %d (%.1f lanes); "
+          "shade passes %d (%.1f lanes)" % (it_all, it_node, ln_node / max(1, it_node), it_leaf,
+                                           ln_leaf / max(1, it_leaf), it_shade, ln_shade / max(1, it_shade)))
 
 
 if __name__ == "__main__":
