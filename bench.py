@@ -75,7 +75,7 @@ def main():
     import grayshift_amd as g
     from grayshift_amd import scenes
 
-    g.set_tuning(a.shade_batch or 56, a.blocks_per_cu or 0, 8 if a.leaf_batch is None else a.leaf_batch,
+    g.set_tuning(a.shade_batch or 52, a.blocks_per_cu or 0, 8 if a.leaf_batch is None else a.leaf_batch,
                  -1 if a.sample_chunk is None else a.sample_chunk)
     sc = scenes.config(a.config, width=a.width, spp=a.spp)
     r = g.Renderer(sc, rank=rank, world_size=world, tile=a.tile)

@@ -464,8 +464,14 @@ __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull <<
 // shares are meaningful, not the absolute time.
 #ifdef GS_STAMPS
 #define GS_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); t = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+// Region timing inside divergent shading code: the first active lane adds the wave's
+// elapsed clock to its wave's LDS slot (one count per wave, whatever the mask).
+#define GS_REGION(k, t0) do { uint64_t t1_; GS_STAMP(t1_); \
+    const uint64_t em_ = __builtin_amdgcn_read_exec(); \
+    if (lane == (uint32_t)__builtin_ctzll(em_)) s_reg[(tid >> 6) * 8 + (k)] += t1_ - (t0); } while (0)
 #else
 #define GS_STAMP(t) do { } while (0)
+#define GS_REGION(k, t0) do { } while (0)
 #endif
 
 // Per-lane pixel state lives in LDS ([field][lane], conflict-free), touched once per
@@ -480,6 +486,10 @@ __host__ __device__ inline size_t lds_bytes(uint32_t stack_depth) {
 __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs A) {
     extern __shared__ __align__(16) uint8_t smem[];
     __shared__ unsigned long long s_cnt[C_N];
+#ifdef GS_STAMPS
+    __shared__ unsigned long long s_reg[(GS_BLOCK / 64) * 8];
+    if (threadIdx.x < (GS_BLOCK / 64) * 8) s_reg[threadIdx.x] = 0;
+#endif
     double* s_d = (double*)smem;                                  // [L_ND][GS_BLOCK]
     uint32_t* s_i = (uint32_t*)(smem + L_ND * 8 * GS_BLOCK);      // [L_NI][GS_BLOCK]
     uint32_t* s_stack = s_i + L_NI * GS_BLOCK;                    // [depth][GS_BLOCK]
@@ -788,16 +798,25 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         if (st == S_SHADE) {
             bool ends = true;
             double Lr = 0.0, Lg = 0.0, Lb = 0.0;
+#ifdef GS_STAMPS
+            uint64_t r0;
+#endif
             if (hit_ref == GS_REF_NONE) {
                 // miss: sample_background (camera.rs:201); the path's only radiance
+                GS_STAMP(r0);
                 const d3 bg = background(sc, ray.d, s_cnt);
+                GS_REGION(0, r0);
                 Lr = Tr * bg.x;
                 Lg = Tg * bg.y;
                 Lb = Tb * bg.z;
             } else {
                 atomicAdd(&s_cnt[C_HITS], 1ull);
+                GS_STAMP(r0);
                 const HitRec h = reconstruct(sc, ray, closest, hit_ref, hit_inst);
+                GS_REGION(1, r0);
+                GS_STAMP(r0);
                 const Scatter s = scatter(sc, h, ray.d, rng, s_cnt);
+                GS_REGION(2, r0);
                 rng = s.rng;
                 if (s.cont) {
                     Tr = Tr * s.col.x;
@@ -807,7 +826,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     if (depth > 0) {
                         ray.o = h.p;
                         ray.d = s.dir;
+                        GS_STAMP(r0);
                         begin_ray();
+                        GS_REGION(3, r0);
                         st = S_TRACE;
                         ends = false;
                     }  // else ray_color(.., 0) = 0 (camera.rs:175): black
@@ -819,8 +840,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 }
             }
             if (ends) {
+                GS_STAMP(r0);
                 add_sample(Lr, Lg, Lb);
                 advance();
+                GS_REGION(4, r0);
             }
         }
 #ifdef GS_STAMPS
@@ -843,6 +866,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         atomicAdd(&dbg[7], (unsigned long long)ln_leaf);
         atomicAdd(&dbg[8], (unsigned long long)it_shade);
         atomicAdd(&dbg[9], (unsigned long long)ln_shade);
+        for (int k = 0; k < 5; k++) atomicAdd(&dbg[10 + k], s_reg[(tid >> 6) * 8 + k]);
     }
 #endif
 #undef LD
@@ -909,7 +933,7 @@ __global__ void gs_unpack_kernel(const float* __restrict__ in, float* __restrict
 
 // =============================================================== host side
 static thread_local std::string tl_err;
-static int32_t g_shade_batch = 56;  // swept on MI355X C4 (chunked): 48 -> 3390, 52 -> 3422, 56 -> 3428, 60 -> 3190 Msamples/s
+static int32_t g_shade_batch = 52;  // swept on MI355X C4 (chunked, uniform loop): 48 -> 3502, 52 -> 3535-3568, 56 -> 3506-3536 Msamples/s
 static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
 static int32_t g_leaf_batch = 8;
 static int32_t g_sample_chunk = -1;  // -1 auto, 0 never split a pixel's samples  // swept on MI355X C4: 0 -> 1940, 8 -> 1986, 16 -> 1923, 32 -> 1770 Msamples/s

@@ -29,7 +29,7 @@ def render(scene, seed=1):
     return out, cnt.as_dict()
 
 
-def set_tuning(shade_batch=56, blocks_per_cu=0, leaf_batch=8, sample_chunk=-1):
+def set_tuning(shade_batch=52, blocks_per_cu=0, leaf_batch=8, sample_chunk=-1):
     """Process-wide launch tuning (see gs_set_tuning in include/grayshift_gpu.h)."""
     N.check(N.lib.gs_set_tuning(shade_batch, blocks_per_cu, leaf_batch, sample_chunk))
 

@@ -11,7 +11,7 @@ def main():
     ap.add_argument("--config", default="C4")
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
-    ap.add_argument("--shade-batch", type=int, default=60)
+    ap.add_argument("--shade-batch", type=int, default=52)
     ap.add_argument("--leaf-batch", type=int, default=8)
     ap.add_argument("--sample-chunk", type=int, default=-1)
     a = ap.parse_args()
@@ -35,6 +35,10 @@ def main():
     print("traversal iterations %d: node passes %d (%.1f active lanes), leaf passes %d (%.1f lanes); "
           "shade passes %d (%.1f lanes)" % (it_all, it_node, ln_node / max(1, it_node), it_leaf,
                                            ln_leaf / max(1, it_leaf), it_shade, ln_shade / max(1, it_shade)))
+    reg = dbg[10:15].cpu().tolist()
+    print("shade regions (%% of shade clock): " + "  ".join(
+        "%s %.1f%%" % (n, 100.0 * x / max(1, v[2])) for n, x in
+        zip(["background", "reconstruct", "scatter", "begin_ray", "sample+advance"], reg)))
 
 
 if __name__ == "__main__":
