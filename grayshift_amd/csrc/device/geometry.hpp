@@ -44,16 +44,59 @@ __device__ __forceinline__ DNode load_node(const DNode* p) {
 // non-NaN values are ever assigned) and IEEE maxNum ignores a NaN operand, as the
 // reference's failed comparison does (a == lo keeps an equal value).  Same for hi.
 // The t0/t1 swap must stay a compare-select: min/max would treat a NaN t1 differently.
+// v_max_f64 / v_min_f64 as they are: IEEE maxNum / minNum, a quiet-NaN operand yields
+// the other one.  fmax/fmin would first "canonicalize" operands the compiler cannot
+// prove are not signalling NaNs (a v_max x,x each); these operands are results of f64
+// arithmetic or the interval bounds, never sNaN, so the bare instruction is the same
+// function.
+__device__ __forceinline__ double hw_max(double a, double b) {
+#ifndef GS_NO_ASM_MINMAX
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return fmax(a, b);
+#endif
+}
+__device__ __forceinline__ double hw_min(double a, double b) {
+#ifndef GS_NO_ASM_MINMAX
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return fmin(a, b);
+#endif
+}
+
+// max(u, b) with a wave-uniform u (tmin) taken as an SGPR-pair operand, so the constant
+// is not rematerialised into VGPRs every traversal step.
+__device__ __forceinline__ double hw_max_u(double u, double b) {
+#ifndef GS_NO_ASM_MINMAX
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "s"(u), "v"(b));
+    return r;
+#else
+    return fmax(u, b);
+#endif
+}
+
 __device__ __forceinline__ void slab(double mn, double mx, double o, double inv, double& lo, double& hi) {
     const double t0 = (mn - o) * inv, t1 = (mx - o) * inv;
     const bool s = t0 < t1;
     const double a = s ? t0 : t1, b = s ? t1 : t0;
-    lo = fmax(lo, a);
-    hi = fmin(hi, b);
+    lo = hw_max(lo, a);
+    hi = hw_min(hi, b);
 }
 __device__ __forceinline__ bool box_hit(const DNode& n, const d3& o, const d3& inv, double tmin, double tmax) {
-    double lo = tmin, hi = tmax;
-    slab(n.mnx, n.mxx, o.x, inv.x, lo, hi);
+    double hi = tmax;
+    double lo;
+    {  // first slab: lo = max(tmin, a) with tmin uniform
+        const double t0 = (n.mnx - o.x) * inv.x, t1 = (n.mxx - o.x) * inv.x;
+        const bool s = t0 < t1;
+        const double a = s ? t0 : t1, b = s ? t1 : t0;
+        lo = hw_max_u(tmin, a);
+        hi = hw_min(hi, b);
+    }
     slab(n.mny, n.mxy, o.y, inv.y, lo, hi);
     slab(n.mnz, n.mxz, o.z, inv.z, lo, hi);
     return !(hi <= lo);
@@ -71,12 +114,17 @@ __device__ __forceinline__ bool fast_slab_ray(const d3& o, const d3& inv) {
 }
 __device__ __forceinline__ void slab_fast(double mn, double mx, double o, double inv, double& lo, double& hi) {
     const double t0 = (mn - o) * inv, t1 = (mx - o) * inv;
-    lo = fmax(lo, fmin(t0, t1));
-    hi = fmin(hi, fmax(t0, t1));
+    lo = hw_max(lo, hw_min(t0, t1));
+    hi = hw_min(hi, hw_max(t0, t1));
 }
 __device__ __forceinline__ bool box_hit_fast(const DNode& n, const d3& o, const d3& inv, double tmin, double tmax) {
-    double lo = tmin, hi = tmax;
-    slab_fast(n.mnx, n.mxx, o.x, inv.x, lo, hi);
+    double hi = tmax;
+    double lo;
+    {
+        const double t0 = (n.mnx - o.x) * inv.x, t1 = (n.mxx - o.x) * inv.x;
+        lo = hw_max_u(tmin, hw_min(t0, t1));
+        hi = hw_min(hi, hw_max(t0, t1));
+    }
     slab_fast(n.mny, n.mxy, o.y, inv.y, lo, hi);
     slab_fast(n.mnz, n.mxz, o.z, inv.z, lo, hi);
     return !(hi <= lo);

@@ -521,7 +521,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     double closest = 0.0;
     bool fast = false;  // this ray's slab times can never be NaN (geometry.hpp box_hit_fast)
     // hot counters kept in registers, flushed per pixel
-    uint32_t c_nodes = 0, c_sph = 0;
+    uint32_t c_nodes = 0, c_sph = 0;  // (per lane: one VALU add beat a 64-bit SALU wave count)
 
     auto begin_ray = [&]() {
         inv = mk(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
