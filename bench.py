@@ -11,8 +11,8 @@ value = all rays traced by all ranks / wall time (max over ranks); a "ray" is on
 world.hit call (camera.rs:177), counted on the device by the very launches timed.
 
 Rank 0 prints ONE JSON line.  At N=1, rank 0 also times the CPU oracle (the
-reference's algorithm restated in C++, oracle/) on a bounded 1/64 pixel subset
-of the same frame: `cpu_baseline`.
+reference's algorithm restated in C++, oracle/) on a bounded subset of the same
+frame (every --cpu-stride-th row and column, ~10 s): `cpu_baseline`.
 """
 import argparse
 import json
@@ -68,6 +68,9 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus %d needs torch.distributed.run with %d ranks" % (a.gpus, a.gpus))
+    if local >= torch.cuda.device_count():
+        raise SystemExit("rank %d: LOCAL_RANK %d but only %d GPUs visible (one GPU per rank)"
+                         % (rank, local, torch.cuda.device_count()))
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -151,7 +154,7 @@ def main():
         cpu = cpu_baseline(sc, a)
 
     traffic = None
-    if a.traffic and os.path.exists(a.traffic):
+    if a.traffic and os.path.exists(a.traffic) and world == 1:  # a 1-GPU whole-frame figure
         with open(a.traffic) as f:
             tj = json.load(f)
         if tj.get("config") == a.config and tj.get("hbm_bytes_per_launch") and a.width is None and a.spp is None:
