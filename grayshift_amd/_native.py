@@ -12,10 +12,11 @@ LIB_PATH = os.environ.get("GS_LIB") or os.path.join(HERE, "libgrayshift.so")  # 
 
 # ------------------------------------------------------------------ enums
 GS_OBJ_SPHERE, GS_OBJ_MOVING_SPHERE, GS_OBJ_QUAD, GS_OBJ_TRIANGLE = 1, 2, 3, 4
-GS_OBJ_LIST, GS_OBJ_BVH, GS_OBJ_TRANSLATE, GS_OBJ_ROTATE_Y, GS_OBJ_CUBE = 5, 6, 7, 8, 9
+GS_OBJ_LIST, GS_OBJ_BVH, GS_OBJ_TRANSLATE, GS_OBJ_ROTATE_Y, GS_OBJ_CUBE, GS_OBJ_MEDIUM = 5, 6, 7, 8, 9, 10
 GS_MAT_LAMBERTIAN, GS_MAT_METAL, GS_MAT_DIELECTRIC, GS_MAT_DIFFUSE_LIGHT, GS_MAT_ISOTROPIC = 1, 2, 3, 4, 5
 GS_TEX_SOLID, GS_TEX_CHECKERED, GS_TEX_IMAGE = 1, 2, 3
 GS_BG_SOLID, GS_BG_HDRI = 1, 2
+GS_ABI_VERSION = 2
 GS_OK, GS_ERR_ARG, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPORTED, GS_ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5
 
 D3 = C.c_double * 3
@@ -66,11 +67,12 @@ class gs_sample_settings(C.Structure):
 
 
 COUNTER_NAMES = ["rays", "node_visits", "sphere_tests", "msphere_tests", "quad_tests", "tri_tests",
-                 "instance_tests", "list_tests", "hits", "image_texels", "hdri_texels", "paths", "pixels"]
+                 "instance_tests", "list_tests", "hits", "image_texels", "hdri_texels", "paths", "pixels",
+                 "medium_tests"]
 
 
 class gs_counters(C.Structure):
-    _fields_ = [(n, C.c_uint64) for n in COUNTER_NAMES] + [("reserved", C.c_uint64 * 3)]
+    _fields_ = [(n, C.c_uint64) for n in COUNTER_NAMES] + [("reserved", C.c_uint64 * 2)]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n in COUNTER_NAMES}
@@ -81,6 +83,10 @@ class gs_camera(C.Structure):
                 ("pad", C.c_uint32), ("center", D3), ("starting_pixel_pos", D3), ("pixel_delta_u", D3),
                 ("pixel_delta_v", D3), ("defocus_angle", C.c_double), ("defocus_disk_u", D3),
                 ("defocus_disk_v", D3)]
+
+
+class gs_medium_rec(C.Structure):  # gs_medium (a flat-scene record)
+    _fields_ = [("boundary", C.c_uint32), ("material", C.c_uint32), ("density_neg_inv", C.c_double)]
 
 
 class gs_partition(C.Structure):
@@ -107,7 +113,8 @@ class gs_flat_scene(C.Structure):
                 ("images", C.c_void_p), ("n_images", C.c_uint32),
                 ("texels8", C.c_void_p), ("n_texels8", C.c_uint64),
                 ("background", gs_background),
-                ("hdri_rgb", C.c_void_p), ("n_hdri_floats", C.c_uint64)]
+                ("hdri_rgb", C.c_void_p), ("n_hdri_floats", C.c_uint64),
+                ("media", C.c_void_p), ("n_media", C.c_uint32)]
 
 
 # Every symbol include/*.h declares, with its ctypes signature.

@@ -61,7 +61,9 @@ enum {
     DM_METAL = 4,         // a = albedo, param = fuzz
     DM_DIELECTRIC = 5,    // param = refraction index
     DM_LIGHT_SOLID = 6,   // a = emitted colour
-    DM_LIGHT_TEX = 7      // `texture`
+    DM_LIGHT_TEX = 7,     // `texture`
+    DM_ISO_SOLID = 8,     // Isotropic over a solid: a = albedo  (material.rs:185-196)
+    DM_ISO_TEX = 9        // Isotropic over `texture`
 };
 struct alignas(16) DMaterial {
     uint32_t kind, texture, needs_uv, pad;
@@ -71,7 +73,7 @@ struct alignas(16) DMaterial {
     double pad2;
 };
 
-enum { C_RAYS = 0, C_NODES, C_SPH, C_MSPH, C_QUAD, C_TRI, C_INST, C_LIST, C_HITS, C_IMG, C_HDRI, C_PATHS, C_PIX, C_N };
+enum { C_RAYS = 0, C_NODES, C_SPH, C_MSPH, C_QUAD, C_TRI, C_INST, C_LIST, C_HITS, C_IMG, C_HDRI, C_PATHS, C_PIX, C_MED, C_N };
 
 struct DevScene {
     const DNode* nodes;
@@ -83,6 +85,7 @@ struct DevScene {
     const gs_list* lists;
     const uint32_t* list_refs;
     const gs_instance* inst;
+    const gs_medium* media;
     const DMaterial* mats;
     const gs_texture* texs;
     const gs_image* images;
@@ -181,31 +184,23 @@ __device__ __forceinline__ void prim_test(const DevScene& sc, uint32_t ref, cons
     }
 }
 
-// The rarer non-node children (everything but a stationary sphere reached directly
-// from a BVH node): moving sphere, quad, triangle, HittableList, Translate/RotateY
-// chain.  Kept out of line so it does not inflate the traversal loop's registers.
-__device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, uint32_t ref, Ray r, double tmin, double closest,
-                                           unsigned long long* cnt) {
-    LeafHit res;
-    res.hit = false;
-    res.t = closest;
-    res.ref = GS_REF_NONE;
-    res.inst = GS_REF_NONE;
-    uint32_t kind = ref >> GS_REF_SHIFT;
-    uint32_t inst_ref = GS_REF_NONE;
-    uint32_t cur = ref;
-    if (kind == GS_REF_INSTANCE) {
-        inst_ref = ref;
+// Translate / RotateY chain (hittable.rs:107-113, :179-193): the ray in the innermost
+// child's space; returns that child's ref.
+__device__ __forceinline__ uint32_t walk_chain(const DevScene& sc, uint32_t cur, Ray& r, unsigned long long* cnt) {
 #pragma unroll 1
-        for (int k = 0; k < GS_MAX_CHAIN && (cur >> GS_REF_SHIFT) == GS_REF_INSTANCE; k++) {
-            const gs_instance& in = sc.inst[cur & GS_REF_MASK];
-            atomicAdd(&cnt[C_INST], 1ull);
-            inst_forward(in, r);
-            cur = in.child;
-        }
-        kind = cur >> GS_REF_SHIFT;
+    for (int k = 0; k < GS_MAX_CHAIN && (cur >> GS_REF_SHIFT) == GS_REF_INSTANCE; k++) {
+        const gs_instance& in = sc.inst[cur & GS_REF_MASK];
+        atomicAdd(&cnt[C_INST], 1ull);
+        inst_forward(in, r);
+        cur = in.child;
     }
-    if (kind == GS_REF_LIST) {
+    return cur;
+}
+
+// A HittableList (hittable.rs:71-86: shrinking closest) or one primitive.
+__device__ __forceinline__ void shape_test(const DevScene& sc, uint32_t cur, const Ray& r, double tmin, double closest,
+                                           uint32_t inst_ref, LeafHit& res, unsigned long long* cnt) {
+    if ((cur >> GS_REF_SHIFT) == GS_REF_LIST) {
         atomicAdd(&cnt[C_LIST], 1ull);
         const gs_list l = sc.lists[cur & GS_REF_MASK];
 #pragma unroll 1
@@ -213,6 +208,66 @@ __device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, uint32_t ref, Ray 
             prim_test(sc, sc.list_refs[l.first + k], r, tmin, res.t, inst_ref, res, cnt);
     } else {
         prim_test(sc, cur, r, tmin, closest, inst_ref, res, cnt);
+    }
+}
+
+// ConstantMedium::hit (volume.rs:32-63): the boundary hit over Interval::UNIVERSE, again
+// from t1 + 0.0001, both clipped to ray_t; then the free-flight distance from the lane's
+// RNG stream, drawn here, inside traversal, in the reference's visit order (:48).
+__device__ __forceinline__ void medium_test(const DevScene& sc, uint32_t cur, const Ray& r, double tmin,
+                                            double closest, uint32_t inst_ref, uint64_t& rng, LeafHit& res,
+                                            unsigned long long* cnt) {
+    atomicAdd(&cnt[C_MED], 1ull);
+    const gs_medium md = sc.media[cur & GS_REF_MASK];
+    const double DMAX = 1.7976931348623157e308;  // f64::MAX; f64::MIN = -f64::MAX
+    LeafHit b1;
+    b1.hit = false;
+    b1.t = DMAX;
+    Ray rb = r;
+    const uint32_t shape = walk_chain(sc, md.boundary, rb, cnt);
+    shape_test(sc, shape, rb, -DMAX, DMAX, GS_REF_NONE, b1, cnt);
+    if (!b1.hit) return;
+    LeafHit b2;
+    b2.hit = false;
+    b2.t = DMAX;
+    rb = r;
+    walk_chain(sc, md.boundary, rb, cnt);  // the second boundary.hit call walks the chain again
+    shape_test(sc, shape, rb, b1.t + 0.0001, DMAX, GS_REF_NONE, b2, cnt);
+    if (!b2.hit) return;
+    double t1 = b1.t, t2 = b2.t;
+    if (t1 < tmin) t1 = tmin;
+    if (t2 > closest) t2 = closest;
+    if (t1 >= t2) return;
+    if (t1 < 0.0) t1 = 0.0;
+    const double ray_len = sqrt(len2(r.d));
+    const double dist_inside_boundary = (t2 - t1) * ray_len;
+    const double hit_dist = md.density_neg_inv * log(wy_f64(rng));
+    if (hit_dist > dist_inside_boundary) return;
+    res.hit = true;
+    res.t = t1 + hit_dist / ray_len;
+    res.ref = cur;
+    res.inst = inst_ref;
+}
+
+// The rarer non-node children (everything but a stationary sphere reached directly
+// from a BVH node): moving sphere, quad, triangle, HittableList, ConstantMedium, behind
+// an optional Translate/RotateY chain.  `rng`: a medium draws from the lane's stream.
+// MEDIA is a kernel template flag: scenes without media compile the medium test out
+// (it costs the traversal loop 4 VGPRs and spills otherwise).
+template <bool MEDIA>
+__device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, uint32_t ref, Ray r, double tmin, double closest,
+                                           uint64_t& rng, unsigned long long* cnt) {
+    LeafHit res;
+    res.hit = false;
+    res.t = closest;
+    res.ref = GS_REF_NONE;
+    res.inst = GS_REF_NONE;
+    const uint32_t inst_ref = (ref >> GS_REF_SHIFT) == GS_REF_INSTANCE ? ref : GS_REF_NONE;
+    const uint32_t cur = walk_chain(sc, ref, r, cnt);
+    if (MEDIA && (cur >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
+        medium_test(sc, cur, r, tmin, closest, inst_ref, rng, res, cnt);
+    } else {
+        shape_test(sc, cur, r, tmin, closest, inst_ref, res, cnt);
     }
     return res;
 }
@@ -280,6 +335,10 @@ __device__ GS_NOINLINE HitRec reconstruct(const DevScene& sc, Ray r, double t, u
         v = dot(ld3(q.w), cross(ld3(q.u), planar));
         outward = ld3(q.normal);
         h.mat = q.material;
+    } else if (kind == GS_REF_MEDIUM) {  // volume.rs:54-62: ray.at(t), normal (1, 0, 0), u = v = 0
+        p = add(r.o, muls(r.d, t));
+        outward = mk(1.0, 0.0, 0.0);
+        h.mat = sc.media[idx].material;
     } else {  // triangle
         const gs_triangle& tr = sc.tris[idx];
         double tt;
@@ -449,6 +508,10 @@ __device__ GS_NOINLINE Scatter scatter(const DevScene& sc, HitRec h, d3 in_dir, 
         s.dir = (cannot_refract || fresnel) ? reflect(ud, h.n) : refract(ud, h.n, ri);
         s.col = mk(1.0, 1.0, 1.0);
         s.cont = 1;
+    } else if (kind == DM_ISO_SOLID || kind == DM_ISO_TEX) {  // Isotropic :185-196
+        s.col = kind == DM_ISO_SOLID ? ld3(m.a) : texture_value(sc, m.texture, h.u, h.v, h.p, cnt);
+        s.dir = random_unit_vector(rng);
+        s.cont = 1;
     } else {  // DiffuseLight :165-169 (emits, never scatters)
         s.col = kind == DM_LIGHT_SOLID ? ld3(m.a) : texture_value(sc, m.texture, h.u, h.v, h.p, cnt);
     }
@@ -483,6 +546,7 @@ __host__ __device__ inline size_t lds_bytes(uint32_t stack_depth) {
     return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4 + (stack_depth + 1) * 4);  // + the dummy slot 0
 }
 
+template <bool MEDIA>
 __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs A) {
     extern __shared__ __align__(16) uint8_t smem[];
     __shared__ unsigned long long s_cnt[C_N];
@@ -767,7 +831,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         hit_inst = GS_REF_NONE;
                     }
                 } else {
-                    const LeafHit lh = leaf_other(sc, cur, ray, tmin, closest, s_cnt);
+                    const LeafHit lh = leaf_other<MEDIA>(sc, cur, ray, tmin, closest, rng, s_cnt);
                     if (lh.hit) {
                         closest = lh.t;
                         hit_ref = lh.ref;
@@ -959,6 +1023,7 @@ struct gs_device_scene {
     uint32_t n_nodes = 0;
     uint32_t stack_depth = 1;  // LDS stack entries per lane (= BVH depth)
     bool fast_boxes = false;  // every node coordinate |x| < 1e300
+    bool has_media = false;   // launch gs_render_kernel<true>
     double* partial = nullptr;  // chunk partial sums, grown on demand
     size_t partial_bytes = 0;
 };
@@ -981,6 +1046,7 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out) {
     auto bad = [](const std::string& m) { return fail(GS_ERR_ARG, "invalid flat scene: " + m); };
     auto unsup = [](const std::string& m) { return fail(GS_ERR_UNSUPPORTED, m); };
     if (!s.nodes && s.n_nodes) return bad("nodes");
+    if (!s.media && s.n_media) return bad("media");
     // the kernel forms node / sphere byte offsets as u32 (ref << 6, ref << 5)
     if (s.n_nodes >= (1u << 26) || s.n_spheres >= (1u << 27)) return unsup("more than 2^26 BVH nodes or 2^27 spheres");
     if (s.n_materials == 0 || !s.materials) return bad("no materials");
@@ -994,8 +1060,8 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out) {
             default: return false;
         }
     };
-    auto leaf_ok = [&](uint32_t r) -> int {  // 0 ok, 1 bad, 2 unsupported
-        uint32_t cur = r;
+    // Walks a Translate/RotateY chain: 0 ok, 1 bad, 2 unsupported (deeper than GS_MAX_CHAIN).
+    auto chain_ok = [&](uint32_t& cur) -> int {
         int chain = 0;
         while ((cur >> GS_REF_SHIFT) == GS_REF_INSTANCE) {
             uint32_t i = cur & GS_REF_MASK;
@@ -1005,17 +1071,38 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out) {
             if (in.kind != GS_INST_TRANSLATE && in.kind != GS_INST_ROTATE_Y) return 1;
             cur = in.child;
         }
-        if ((cur >> GS_REF_SHIFT) == GS_REF_LIST) {
+        return 0;
+    };
+    // A list of primitives or one primitive (what walk_chain may end in).
+    auto shape_ok = [&](uint32_t cur) -> int {
+        const uint32_t k = cur >> GS_REF_SHIFT;
+        if (k == GS_REF_LIST) {
             uint32_t i = cur & GS_REF_MASK;
             if (i >= s.n_lists) return 1;
             const gs_list& l = s.lists[i];
             if ((uint64_t)l.first + l.count > s.n_list_refs) return 1;
-            for (uint32_t k = 0; k < l.count; k++)
-                if (!prim_ok(s.list_refs[l.first + k])) return 2;
+            for (uint32_t q = 0; q < l.count; q++)
+                if (!prim_ok(s.list_refs[l.first + q])) return 2;
             return 0;
         }
-        if ((cur >> GS_REF_SHIFT) == GS_REF_NODE) return chain ? 2 : 1;
+        if (k == GS_REF_NODE || k == GS_REF_MEDIUM || k == GS_REF_INSTANCE) return 2;
         return prim_ok(cur) ? 0 : 1;
+    };
+    auto leaf_ok = [&](uint32_t r) -> int {  // 0 ok, 1 bad, 2 unsupported
+        uint32_t cur = r;
+        int e = chain_ok(cur);
+        if (e) return e;
+        if ((cur >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
+            uint32_t i = cur & GS_REF_MASK;
+            if (i >= s.n_media || !s.media) return 1;
+            if (s.media[i].material >= s.n_materials) return 1;
+            uint32_t b = s.media[i].boundary;
+            e = chain_ok(b);
+            if (e) return e;
+            return shape_ok(b);
+        }
+        if ((cur >> GS_REF_SHIFT) == GS_REF_NODE) return cur != r ? 2 : 1;
+        return shape_ok(cur);
     };
     // Walk the tree from the root: indices in range, no node reached twice, depth bound.
     std::vector<uint8_t> seen(s.n_nodes, 0);
@@ -1037,8 +1124,8 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out) {
         } else {
             int e = leaf_ok(r);
             if (e == 1) return bad("leaf reference");
-            if (e == 2) return unsup("instance chain deeper than 4, BVH under an instance, or a list member "
-                                     "that is not a primitive");
+            if (e == 2) return unsup("instance chain deeper than 4, BVH under an instance or inside a medium "
+                                     "boundary, nested media, or a list member that is not a primitive");
         }
     }
     if (maxd > GS_STACK) return unsup("BVH deeper than the device stack (" + std::to_string(GS_STACK) + ")");
@@ -1050,10 +1137,8 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out) {
     for (uint32_t i = 0; i < s.n_triangles; i++) if (!mat_ok(s.triangles[i].material)) return bad("triangle material");
     for (uint32_t i = 0; i < s.n_materials; i++) {
         const gs_material& m = s.materials[i];
-        if (m.kind == GS_MAT_LAMBERTIAN || m.kind == GS_MAT_DIFFUSE_LIGHT) {
+        if (m.kind == GS_MAT_LAMBERTIAN || m.kind == GS_MAT_DIFFUSE_LIGHT || m.kind == GS_MAT_ISOTROPIC) {
             if (m.texture >= s.n_textures) return bad("material texture");
-        } else if (m.kind == GS_MAT_ISOTROPIC) {
-            return unsup("Isotropic material (volumes) on the device path");
         } else if (m.kind != GS_MAT_METAL && m.kind != GS_MAT_DIELECTRIC) {
             return bad("material kind");
         }
@@ -1166,7 +1251,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         const gs_material& m = s->materials[i];
         DMaterial d{};
         d.texture = m.texture;
-        const bool textured = m.kind == GS_MAT_LAMBERTIAN || m.kind == GS_MAT_DIFFUSE_LIGHT;
+        const bool textured = m.kind == GS_MAT_LAMBERTIAN || m.kind == GS_MAT_DIFFUSE_LIGHT || m.kind == GS_MAT_ISOTROPIC;
         d.needs_uv = textured ? tex_needs_uv(*s, m.texture) : 0;
         if (textured) {
             const gs_texture& t = s->textures[m.texture];
@@ -1175,6 +1260,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                                   s->textures[t.odd].kind == GS_TEX_SOLID;
             if (m.kind == GS_MAT_LAMBERTIAN) {
                 d.kind = solid ? DM_LAMB_SOLID : (checker2 ? DM_LAMB_CHECKER : DM_LAMB_TEX);
+            } else if (m.kind == GS_MAT_ISOTROPIC) {
+                d.kind = solid ? DM_ISO_SOLID : DM_ISO_TEX;
             } else {
                 d.kind = solid ? DM_LIGHT_SOLID : DM_LIGHT_TEX;
             }
@@ -1215,6 +1302,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     size_t o_list = L.add(s->lists, s->n_lists * sizeof(gs_list));
     size_t o_lref = L.add(s->list_refs, s->n_list_refs * 4);
     size_t o_inst = L.add(s->instances, s->n_instances * sizeof(gs_instance));
+    size_t o_media = L.add(s->media, s->n_media * sizeof(gs_medium));
     size_t o_mat = L.add(mats.data(), mats.size() * sizeof(DMaterial));
     size_t o_tex = L.add(s->textures, s->n_textures * sizeof(gs_texture));
     size_t o_img = L.add(s->images, s->n_images * sizeof(gs_image));
@@ -1248,6 +1336,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     d.lists = (const gs_list*)(b + o_list);
     d.list_refs = (const uint32_t*)(b + o_lref);
     d.inst = (const gs_instance*)(b + o_inst);
+    d.media = (const gs_medium*)(b + o_media);
     d.mats = (const DMaterial*)(b + o_mat);
     d.texs = (const gs_texture*)(b + o_tex);
     d.images = (const gs_image*)(b + o_img);
@@ -1260,6 +1349,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ds->params = (KParams*)(b + o_params);
     ds->n_nodes = s->n_nodes;
     ds->stack_depth = depth < 1 ? 1 : depth;
+    ds->has_media = s->n_media != 0;
     ds->fast_boxes = true;
     for (uint32_t i = 0; i < s->n_nodes && ds->fast_boxes; i++)
         for (int k = 0; k < 3; k++)
@@ -1372,7 +1462,8 @@ gs_status gs_render_tiles_debug_async(const gs_device_scene* ds, const gs_camera
     int per_cu = g_blocks_per_cu;
     if (per_cu <= 0) {
         int occ = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gs_render_kernel, GS_BLOCK, lds));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &occ, ds->has_media ? gs_render_kernel<true> : gs_render_kernel<false>, GS_BLOCK, lds));
         per_cu = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
     }
     int64_t blocks = (int64_t)cus * per_cu;
@@ -1380,7 +1471,10 @@ gs_status gs_render_tiles_debug_async(const gs_device_scene* ds, const gs_camera
     int64_t max_blocks = ((int64_t)kp.n_items + GS_BLOCK - 1) / GS_BLOCK;
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(gs_render_kernel, dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
+    if (ds->has_media)
+        hipLaunchKernelGGL(gs_render_kernel<true>, dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
+    else
+        hipLaunchKernelGGL(gs_render_kernel<false>, dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
     if (chunk) {
         const unsigned grid = (unsigned)std::min<int64_t>((cap + 255) / 256, 8192);

@@ -71,6 +71,8 @@ struct SpecBuilder {
             case GS_OBJ_BVH: return BVHNode::construct_tree(children());
             case GS_OBJ_TRANSLATE: return std::make_unique<Translate>(object(o.first, depth + 1), Vec3(p[0], p[1], p[2]));
             case GS_OBJ_ROTATE_Y: return std::make_unique<RotateY>(object(o.first, depth + 1), p[0]);
+            case GS_OBJ_MEDIUM:
+                return std::make_unique<ConstantMedium>(object(o.first, depth + 1), p[0], material(o.material));
             default: throw std::invalid_argument("unknown object kind");
         }
     }
@@ -83,8 +85,7 @@ struct SpecBuilder {
                 case GS_MAT_METAL: mat.push_back(std::make_shared<Metal>(Vec3(m.p[0], m.p[1], m.p[2]), m.p[3])); break;
                 case GS_MAT_DIELECTRIC: mat.push_back(std::make_shared<Dielectric>(m.p[0])); break;
                 case GS_MAT_DIFFUSE_LIGHT: mat.push_back(std::make_shared<DiffuseLight>(texture(m.texture))); break;
-                case GS_MAT_ISOTROPIC:
-                    throw std::domain_error("Isotropic (volumes) is not supported on the device path");
+                case GS_MAT_ISOTROPIC: mat.push_back(std::make_shared<Isotropic>(texture(m.texture))); break;
                 default: throw std::invalid_argument("unknown material kind");
             }
         }
@@ -243,7 +244,7 @@ int64_t gs_host_struct_size(const char* name) {
     GS_SZ(gs_object) GS_SZ(gs_material_spec) GS_SZ(gs_texture_spec) GS_SZ(gs_image_spec)
     GS_SZ(gs_background_spec) GS_SZ(gs_scene_spec) GS_SZ(gs_camera_spec) GS_SZ(gs_sample_settings)
     GS_SZ(gs_counters) GS_SZ(gs_node) GS_SZ(gs_sphere) GS_SZ(gs_msphere) GS_SZ(gs_quad) GS_SZ(gs_triangle)
-    GS_SZ(gs_list) GS_SZ(gs_instance) GS_SZ(gs_material) GS_SZ(gs_texture) GS_SZ(gs_image)
+    GS_SZ(gs_list) GS_SZ(gs_instance) GS_SZ(gs_medium) GS_SZ(gs_material) GS_SZ(gs_texture) GS_SZ(gs_image)
     GS_SZ(gs_background) GS_SZ(gs_flat_scene) GS_SZ(gs_camera) GS_SZ(gs_partition)
 #undef GS_SZ
     return -1;

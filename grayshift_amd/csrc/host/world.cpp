@@ -229,6 +229,14 @@ uint32_t DiffuseLight::flatten(Flattener& f) const {
     return (uint32_t)s;
 }
 
+uint32_t Isotropic::flatten(Flattener& f) const {
+    size_t s = slot_of(f.mat_keys, this);
+    uint32_t tex = f.texture_index(texture.get());
+    f.materials[s].kind = GS_MAT_ISOTROPIC;
+    f.materials[s].texture = tex;
+    return (uint32_t)s;
+}
+
 uint32_t Sphere::flatten(Flattener& f) const {
     uint32_t m = f.material_index(material.get());
     if (!is_moving) {
@@ -322,6 +330,7 @@ uint32_t RotateY::flatten(Flattener& f) const {
 }
 uint32_t BVHNode::flatten(Flattener& f) const {
     if (f.inside_instance) throw std::domain_error("BVH under Translate/RotateY is not supported on the device path");
+    if (f.inside_medium) throw std::domain_error("BVH as a ConstantMedium boundary is not supported on the device path");
     // Pre-order: the left subtree follows its parent in memory (cache locality).
     size_t idx = f.nodes.size();
     check_index(idx, "nodes");
@@ -339,6 +348,23 @@ uint32_t BVHNode::flatten(Flattener& f) const {
     return GS_MAKE_REF(GS_REF_NODE, idx);
 }
 
+uint32_t ConstantMedium::flatten(Flattener& f) const {  // volume.rs:10-29
+    if (f.inside_medium)
+        throw std::domain_error("ConstantMedium inside a ConstantMedium boundary is not supported on the device path");
+    size_t idx = f.media.size();
+    check_index(idx, "media");
+    f.media.push_back(gs_medium{});
+    f.inside_medium = true;
+    uint32_t b = boundary->flatten(f);
+    f.inside_medium = false;
+    uint32_t m = f.material_index(phase_function.get());
+    gs_medium& md = f.media[idx];
+    md.boundary = b;
+    md.material = m;
+    md.density_neg_inv = density_neg_inv;
+    return GS_MAKE_REF(GS_REF_MEDIUM, idx);
+}
+
 void FlatScene::finalize(uint32_t root, const Background& bg) {
     gs_flat_scene& v = view;
     std::memset(&v, 0, sizeof(v));
@@ -352,6 +378,7 @@ void FlatScene::finalize(uint32_t root, const Background& bg) {
     v.lists = f.lists.data();           v.n_lists = (uint32_t)f.lists.size();
     v.list_refs = f.list_refs.data();   v.n_list_refs = (uint32_t)f.list_refs.size();
     v.instances = f.instances.data();   v.n_instances = (uint32_t)f.instances.size();
+    v.media = f.media.data();           v.n_media = (uint32_t)f.media.size();
     v.materials = f.materials.data();   v.n_materials = (uint32_t)f.materials.size();
     v.textures = f.textures.data();     v.n_textures = (uint32_t)f.textures.size();
     v.images = f.images.data();         v.n_images = (uint32_t)f.images.size();

@@ -163,6 +163,16 @@ public:
     TexturePtr texture;
 };
 
+class Isotropic : public Material {  // material.rs:171-200 (phase function of a ConstantMedium)
+public:
+    explicit Isotropic(TexturePtr t) : texture(std::move(t)) {}
+    static std::shared_ptr<Isotropic> from_color(Vec3 c) {
+        return std::make_shared<Isotropic>(std::make_shared<SolidColorTexture>(c));
+    }
+    uint32_t flatten(Flattener& f) const override;
+    TexturePtr texture;
+};
+
 // --------------------------------------------------------------- hittables
 class Hittable {
 public:
@@ -250,6 +260,22 @@ public:
     AABB bbox;
 };
 
+// hittable/volume.rs:10-68.  The boundary is any Hittable but a BVH or another medium
+// on the device path (flatten throws std::domain_error otherwise).
+class ConstantMedium : public Hittable {
+public:
+    ConstantMedium(HittablePtr boundary, double density, MaterialPtr phase_function)
+        : boundary(std::move(boundary)), density_neg_inv(-1.0 / density), phase_function(std::move(phase_function)) {}
+    static std::unique_ptr<ConstantMedium> from_isotropic_color(HittablePtr boundary, double density, Vec3 color) {
+        return std::make_unique<ConstantMedium>(std::move(boundary), density, Isotropic::from_color(color));
+    }
+    AABB bounding_box() const override { return boundary->bounding_box(); }
+    uint32_t flatten(Flattener& f) const override;
+    HittablePtr boundary;
+    double density_neg_inv;
+    MaterialPtr phase_function;
+};
+
 // ------------------------------------------------------------------ camera
 struct SampleSettings {  // camera.rs:239-244
     double confidence, tolerance;
@@ -284,6 +310,7 @@ public:
     std::vector<gs_list> lists;
     std::vector<uint32_t> list_refs;
     std::vector<gs_instance> instances;
+    std::vector<gs_medium> media;
     std::vector<gs_material> materials;
     std::vector<gs_texture> textures;
     std::vector<gs_image> images;
@@ -293,6 +320,7 @@ public:
     std::vector<const ImageTexture*> img_keys;
     uint32_t depth = 0, max_depth = 0;  // BVH node nesting while flattening
     bool inside_instance = false;
+    bool inside_medium = false;  // flattening a ConstantMedium boundary
 };
 
 // A flattened world + background, ready for gs_render / gs_device_scene_create.

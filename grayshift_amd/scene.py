@@ -3,7 +3,8 @@
 Mirrors the construction calls of the reference's scene builders (src/main.rs):
 ``Sphere::new_stationary``, ``Quad::new``, ``Quad::cube``, ``RotateY::new``,
 ``Translate::new``, ``Lambertian::from_color`` / ``from_texture``, ``Metal::new``,
-``Dielectric::new``, ``DiffuseLight::from_color``, ``CheckeredTexture::from_colors``,
+``Dielectric::new``, ``DiffuseLight::from_color``, ``Isotropic::from_color``,
+``ConstantMedium::new`` / ``from_isotropic_color``, ``CheckeredTexture::from_colors``,
 ``ImageTexture::new``, ``world.add``.  The result is a gs_scene_spec that both the
 product host (C++) and the CPU oracle consume; neither side sees the other's world.
 """
@@ -98,6 +99,12 @@ class SceneBuilder:
     def diffuse_light(self, rgb):  # DiffuseLight::from_color
         return self._mat(N.GS_MAT_DIFFUSE_LIGHT, self.solid(rgb))
 
+    def isotropic_texture(self, tex):  # Isotropic::new (material.rs:176-178)
+        return self._mat(N.GS_MAT_ISOTROPIC, tex)
+
+    def isotropic(self, rgb):  # Isotropic::from_color (material.rs:180-182)
+        return self._mat(N.GS_MAT_ISOTROPIC, self.solid(rgb))
+
     # -------------------------------------------------------------- objects
     def _obj(self, kind, material=-1, first=-1, count=0, p=()):
         o = N.gs_object(kind=kind, material=material, first=first, count=count)
@@ -137,6 +144,12 @@ class SceneBuilder:
 
     def rotate_y(self, obj, angle_degrees):
         return self._obj(N.GS_OBJ_ROTATE_Y, first=obj, p=(angle_degrees,))
+
+    def medium(self, boundary, density, phase_material):  # ConstantMedium::new (volume.rs:17-21)
+        return self._obj(N.GS_OBJ_MEDIUM, phase_material, first=boundary, p=(density,))
+
+    def medium_isotropic(self, boundary, density, rgb):  # ConstantMedium::from_isotropic_color (:23-28)
+        return self.medium(boundary, density, self.isotropic(rgb))
 
     def add(self, obj):  # world.add
         self._world.append(int(obj))

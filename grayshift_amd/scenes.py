@@ -170,6 +170,18 @@ def cornell_box(width=600, settings=None):  # main.rs:421-517
     return Scene("cornell_box", b.build(), cam, settings or sample_settings(0.95, 0.5, 32, 1000))
 
 
+def cornell_smoke(width=600, settings=None):  # main.rs:519-624
+    b = SceneBuilder()
+    white = _cornell_walls(b, (113.0, 554.0, 127.0), (330.0, 0.0, 0.0), (0.0, 0.0, 305.0), (7.0, 7.0, 7.0))
+    box1 = b.cube((0.0, 0.0, 0.0), (165.0, 330.0, 165.0), white)
+    b.add(b.medium_isotropic(b.translate(b.rotate_y(box1, 15.0), (265.0, 0.0, 295.0)), 0.01, (0.0, 0.0, 0.0)))
+    box2 = b.cube((0.0, 0.0, 0.0), (165.0, 165.0, 165.0), white)
+    b.add(b.medium_isotropic(b.translate(b.rotate_y(box2, -18.0), (130.0, 0.0, 65.0)), 0.01, (1.0, 1.0, 1.0)))
+    b.background_solid((0.0, 0.0, 0.0))
+    cam = _camera(1.0, width, 50, 40.0, (278.0, 278.0, -800.0), (278.0, 278.0, 0.0), (0.0, 1.0, 0.0), 0.0, 10.0)
+    return Scene("cornell_smoke", b.build(), cam, settings or sample_settings(0.95, 0.25, 32, 1000))
+
+
 def hdri(width=600, settings=None):  # main.rs:792-834 — the literal default (SCENE = 11)
     b = SceneBuilder()
     b.add(b.sphere((4.0, 1.0, 0.0), 1.0, b.metal((0.7, 0.6, 0.5), 0.0)))
@@ -228,6 +240,7 @@ SCENES = {
     "earth_hdr": lambda width=400, settings=None: earth(width, settings, hdri=True),
     "quads": quads,
     "cornell_box": cornell_box,
+    "cornell_smoke": cornell_smoke,
     "hdri": hdri,
     "triangles": triangles,
     "mixed": mixed,

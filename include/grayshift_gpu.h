@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 1
+#define GS_ABI_VERSION 2
 
 typedef int32_t gs_status;
 enum {
@@ -48,7 +48,8 @@ enum gs_ref_kind {
     GS_REF_QUAD = 4,     /* Quad                          -> quads[]     */
     GS_REF_TRIANGLE = 5, /* Triangle                      -> triangles[] */
     GS_REF_LIST = 6,     /* HittableList of primitives    -> lists[]     */
-    GS_REF_INSTANCE = 7  /* Translate / RotateY           -> instances[] */
+    GS_REF_INSTANCE = 7, /* Translate / RotateY           -> instances[] */
+    GS_REF_MEDIUM = 8    /* ConstantMedium                -> media[]     */
 };
 #define GS_MAKE_REF(kind, idx) (((uint32_t)(kind) << GS_REF_SHIFT) | ((uint32_t)(idx) & GS_REF_MASK))
 
@@ -109,10 +110,18 @@ typedef struct gs_instance {
     double p[3]; /* TRANSLATE: offset; ROTATE_Y: sin_theta, cos_theta, 0 */
 } gs_instance;
 
+/* ConstantMedium (hittable/volume.rs:10-29): 16 B.  boundary: an instance chain, a list
+ * or a primitive (no BVH, no medium); material: the phase function (any material). */
+typedef struct gs_medium {
+    uint32_t boundary;
+    uint32_t material;
+    double density_neg_inv; /* -1 / density (volume.rs:18) */
+} gs_medium;
+
 /* Material record (material.rs): 40 B. */
 typedef struct gs_material {
     uint32_t kind;    /* gs_mat_kind */
-    uint32_t texture; /* LAMBERTIAN / DIFFUSE_LIGHT */
+    uint32_t texture; /* LAMBERTIAN / DIFFUSE_LIGHT / ISOTROPIC */
     double albedo[3]; /* METAL */
     double param;     /* METAL: fuzz; DIELECTRIC: refraction_index */
 } gs_material;
@@ -159,6 +168,7 @@ typedef struct gs_flat_scene {
     const uint8_t* texels8;       uint64_t n_texels8;  /* bytes */
     gs_background background;
     const float* hdri_rgb;        uint64_t n_hdri_floats; /* width*height*3 */
+    const gs_medium* media;       uint32_t n_media;       /* (ABI 2) */
 } gs_flat_scene;
 
 /* The fields `Camera::new` derives (camera.rs:17-98), computed by the host. */

@@ -30,7 +30,9 @@ enum gs_obj_kind {
     GS_OBJ_BVH           = 6, /* BVHNode::from_list      BVH.rs:15      children[first .. first+count)       */
     GS_OBJ_TRANSLATE     = 7, /* Translate::new          hittable.rs:99 child = first; p: offset[3]          */
     GS_OBJ_ROTATE_Y      = 8, /* RotateY::new            hittable.rs:135 child = first; p: angle (degrees)   */
-    GS_OBJ_CUBE          = 9  /* Quad::cube              quad.rs:54     p: point_a[3], point_b[3] (a list)   */
+    GS_OBJ_CUBE          = 9, /* Quad::cube              quad.rs:54     p: point_a[3], point_b[3] (a list)   */
+    GS_OBJ_MEDIUM        = 10 /* ConstantMedium::new     volume.rs:17   boundary = first, phase function =
+                                 material; p: density                                                      */
 };
 
 typedef struct gs_object {
@@ -46,7 +48,7 @@ enum gs_mat_kind {
     GS_MAT_METAL         = 2, /* material.rs:75  p: albedo[3], fuzz             */
     GS_MAT_DIELECTRIC    = 3, /* material.rs:105 p: refraction_index            */
     GS_MAT_DIFFUSE_LIGHT = 4, /* material.rs:151 texture                        */
-    GS_MAT_ISOTROPIC     = 5  /* material.rs:171 texture (volumes: not on GPU)  */
+    GS_MAT_ISOTROPIC     = 5  /* material.rs:171 texture (phase function of a ConstantMedium) */
 };
 
 typedef struct gs_material_spec {
@@ -135,7 +137,8 @@ typedef struct gs_counters {
     uint64_t hdri_texels;     /* HDRI::sample                  camera.rs:257 */
     uint64_t paths;           /* camera samples (get_ray calls)              */
     uint64_t pixels;          /* pixels finished                             */
-    uint64_t reserved[3];
+    uint64_t medium_tests;    /* ConstantMedium::hit           volume.rs:32  */
+    uint64_t reserved[2];
 } gs_counters;
 
 #ifdef __cplusplus

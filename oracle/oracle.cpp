@@ -562,6 +562,33 @@ struct BVHNode : Hittable { /* hittable/BVH.rs */
     AABB bounding_box() const override { return bbox; }
 };
 
+struct ConstantMedium : Hittable { /* hittable/volume.rs:10-68 */
+    HittablePtr boundary;
+    double density_neg_inv;
+    const Material* phase_function;
+    ConstantMedium(HittablePtr b, double density, const Material* m) /* :17-21 */
+        : boundary(std::move(b)), density_neg_inv(-1.0 / density), phase_function(m) {}
+    bool hit(const Ray& ray, Interval ray_t, HitRecord& rec) const override { /* :32-63 */
+        tl_cnt.medium_tests++;
+        HitRecord r1, r2;
+        if (!boundary->hit(ray, Interval::UNIVERSE(), r1)) return false;
+        if (!boundary->hit(ray, Interval(r1.t + 0.0001, DBL_MAX), r2)) return false;
+        double t1 = r1.t, t2 = r2.t;
+        if (t1 < ray_t.min) t1 = ray_t.min;
+        if (t2 > ray_t.max) t2 = ray_t.max;
+        if (t1 >= t2) return false;
+        if (t1 < 0.0) t1 = 0.0;
+        double ray_len = ray.direction.length();
+        double dist_inside_boundary = (t2 - t1) * ray_len;
+        double hit_dist = density_neg_inv * std::log(rand_f64()); /* the RNG draw inside traversal (:48) */
+        if (hit_dist > dist_inside_boundary) return false;
+        double t = t1 + hit_dist / ray_len;
+        rec = HitRecord::make(ray, t, ray.at(t), Vec3(1.0, 0.0, 0.0), phase_function, 0.0, 0.0);
+        return true;
+    }
+    AABB bounding_box() const override { return boundary->bounding_box(); } /* :65-67 */
+};
+
 /* ------------------------------------------------------------ Material ---- */
 /* material.rs */
 struct ScatterRecord {
@@ -902,6 +929,7 @@ static HittablePtr build_object(const gs_scene_spec& s, int idx, const std::vect
         }
         case GS_OBJ_TRANSLATE: return std::make_unique<Translate>(build_object(s, o.first, mats), Vec3(p[0], p[1], p[2]));
         case GS_OBJ_ROTATE_Y: return std::make_unique<RotateY>(build_object(s, o.first, mats), p[0]);
+        case GS_OBJ_MEDIUM: return std::make_unique<ConstantMedium>(build_object(s, o.first, mats), p[0], mat());
         default: throw std::runtime_error("unknown object kind");
     }
 }

@@ -34,6 +34,8 @@ GOLDEN = {
     "hdri_adaptive": ("hdri", {}, 32, None),
     "cornell_adaptive": ("cornell_box", {}, 24, None),
     "bouncing_adaptive": ("bouncing_spheres", {"grid": 11}, 32, None),
+    "cornell_smoke": ("cornell_smoke", {}, 24, 8),
+    "smoke_adaptive": ("cornell_smoke", {}, 16, None),
 }
 
 

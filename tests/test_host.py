@@ -39,7 +39,7 @@ def test_every_declared_symbol_is_exported(built):
 
 
 def test_version_and_error_channel():
-    assert N.lib.gs_version() == 1
+    assert N.lib.gs_version() == N.GS_ABI_VERSION == 2
     assert N.lib.gs_set_tuning(0, 0, 0, -1) == N.GS_ERR_ARG
     assert b"tuning" in N.lib.gs_last_error()
     assert N.lib.gs_set_tuning(60, 0, 0, -1) == N.GS_OK
@@ -57,11 +57,12 @@ def test_struct_layouts_match(name):
 def test_device_record_sizes():
     # the per-unit record sizes DESIGN.md §5 prices
     for name, size in [("gs_node", 64), ("gs_sphere", 40), ("gs_msphere", 64), ("gs_quad", 136),
-                       ("gs_triangle", 104), ("gs_instance", 32), ("gs_material", 40)]:
+                       ("gs_triangle", 104), ("gs_instance", 32), ("gs_medium", 16), ("gs_material", 40)]:
         assert N.lib.gs_host_struct_size(name.encode()) == size, name
 
 
-ALL_SCENES = ["C1", "C3", "C4", "C5", "earth", "quads", "triangles", "checkered_spheres", "hdri", "cornell_box"]
+ALL_SCENES = ["C1", "C3", "C4", "C5", "earth", "quads", "triangles", "checkered_spheres", "hdri", "cornell_box",
+              "cornell_smoke"]
 
 
 def _scene(name):
@@ -171,10 +172,30 @@ def test_malformed_scene_is_rejected_before_the_device():
     assert N.lib.gs_device_scene_create(C.byref(f), C.byref(out)) == N.GS_ERR_ARG
 
 
-def test_volume_material_is_unsupported():
+def test_media_flatten_to_medium_records():
+    """cornell_smoke (main.rs:519-624): two ConstantMedium over Translate(RotateY(cube))."""
+    hs = g.HostScene(scenes.cornell_smoke(width=32).spec)
+    f = hs.flat
+    assert f.n_media == 2
+    recs = (N.gs_medium_rec * 2).from_address(f.media)
+    for r in recs:
+        assert r.boundary >> 28 == 7  # an instance chain (Translate)
+        assert r.density_neg_inv == -1.0 / 0.01
+    hs.close()
+
+
+@pytest.mark.parametrize("case", ["bvh_boundary", "nested_medium", "medium_in_list"])
+def test_unsupported_media_are_rejected(case):
     b = SceneBuilder()
-    m = b._mat(N.GS_MAT_ISOTROPIC, b.solid((1, 1, 1)))
-    b.add(b.sphere((0, 0, 0), 1, m))
+    m = b.lambertian((1, 1, 1))
+    iso = b.isotropic((1, 1, 1))
+    s1, s2, s3 = (b.sphere((3.0 * k, 0, 0), 1, m) for k in range(3))
+    if case == "bvh_boundary":
+        b.add(b.medium(b.bvh([s1, s2, s3]), 0.5, iso))
+    elif case == "nested_medium":
+        b.add(b.medium(b.medium(s1, 0.5, iso), 0.5, iso))
+    else:
+        b.add(b.hittable_list([b.medium(s1, 0.5, iso), s2]))
     h = C.c_void_p()
     assert N.lib.gs_host_scene_from_spec(b.build().ptr(), C.byref(h)) == N.GS_ERR_UNSUPPORTED
 
