@@ -12,7 +12,7 @@ import importlib
 
 _EXPORTS = {
     "HostScene": "renderer", "Renderer": "renderer", "camera": "renderer", "render": "renderer",
-    "set_tuning": "renderer", "write_ppm": "renderer",
+    "set_tuning": "renderer", "write_ppm": "renderer", "render_ppm": "renderer", "ppm_encode_async": "renderer",
     "SceneBuilder": "scene", "camera_spec": "scene", "fixed_spp": "scene", "sample_settings": "scene",
 }
 _SUBMODULES = {"scenes", "partition", "assets", "_native", "scene"}

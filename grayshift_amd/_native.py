@@ -16,7 +16,7 @@ GS_OBJ_LIST, GS_OBJ_BVH, GS_OBJ_TRANSLATE, GS_OBJ_ROTATE_Y, GS_OBJ_CUBE, GS_OBJ_
 GS_MAT_LAMBERTIAN, GS_MAT_METAL, GS_MAT_DIELECTRIC, GS_MAT_DIFFUSE_LIGHT, GS_MAT_ISOTROPIC = 1, 2, 3, 4, 5
 GS_TEX_SOLID, GS_TEX_CHECKERED, GS_TEX_IMAGE = 1, 2, 3
 GS_BG_SOLID, GS_BG_HDRI = 1, 2
-GS_ABI_VERSION = 2
+GS_ABI_VERSION = 3
 GS_OK, GS_ERR_ARG, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPORTED, GS_ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5
 
 D3 = C.c_double * 3
@@ -117,6 +117,10 @@ class gs_flat_scene(C.Structure):
                 ("media", C.c_void_p), ("n_media", C.c_uint32)]
 
 
+class gs_render_outputs(C.Structure):
+    _fields_ = [("rgb", C.c_void_p), ("rgb8", C.c_void_p), ("item_visits", C.c_void_p)]
+
+
 # Every symbol include/*.h declares, with its ctypes signature.
 _P = C.c_void_p
 SIGNATURES = {
@@ -133,6 +137,15 @@ SIGNATURES = {
                                                 C.POINTER(gs_partition), _P, _P, _P, _P]),
     "gs_unpack_tiles_async": (C.c_int32, [C.POINTER(gs_camera), C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P, _P,
                                           _P]),
+    "gs_render_tiles_ex_async": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64,
+                                             C.POINTER(gs_partition), C.POINTER(gs_render_outputs), _P, _P]),
+    "gs_unpack_tiles_u8_async": (C.c_int32, [C.POINTER(gs_camera), C.c_int32, C.c_int32, C.c_int32, C.c_int64, _P,
+                                             _P, _P]),
+    "gs_ppm_max_bytes": (C.c_int64, [C.c_int32, C.c_int32]),
+    "gs_ppm_scratch_bytes": (C.c_int64, [C.c_int32, C.c_int32]),
+    "gs_ppm_encode_async": (C.c_int32, [_P, C.c_int32, C.c_int32, _P, C.c_int64, _P, _P, C.c_int64, _P]),
+    "gs_render_ppm": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64, _P,
+                                  C.c_int64, C.POINTER(C.c_int64), C.POINTER(gs_counters)]),
     "gs_render": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64, _P,
                               C.POINTER(gs_counters)]),
     # grayshift_host.h
@@ -142,6 +155,9 @@ SIGNATURES = {
     "gs_host_camera": (C.c_int32, [C.POINTER(gs_camera_spec), C.POINTER(gs_camera)]),
     "gs_host_render_spec": (C.c_int32, [C.POINTER(gs_scene_spec), C.POINTER(gs_camera_spec),
                                         C.POINTER(gs_sample_settings), C.c_uint64, _P, C.POINTER(gs_counters)]),
+    "gs_host_render_ppm_spec": (C.c_int32, [C.POINTER(gs_scene_spec), C.POINTER(gs_camera_spec),
+                                            C.POINTER(gs_sample_settings), C.c_uint64, _P, C.c_int64,
+                                            C.POINTER(C.c_int64), C.POINTER(gs_counters)]),
     "gs_host_write_ppm": (C.c_int32, [C.c_char_p, C.c_int32, C.c_int32, _P]),
     "gs_host_color_byte": (C.c_int32, [C.c_double]),
     "gs_host_bvh_topology": (C.c_int64, [C.POINTER(gs_scene_spec), C.POINTER(C.c_int32), C.c_int64]),

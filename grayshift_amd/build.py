@@ -23,6 +23,7 @@ ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
 
 SOURCES = [
     os.path.join(HERE, "csrc", "device", "render.hip"),
+    os.path.join(HERE, "csrc", "device", "output.hip"),
     os.path.join(HERE, "csrc", "host", "world.cpp"),
     os.path.join(HERE, "csrc", "host", "camera.cpp"),
     os.path.join(HERE, "csrc", "host", "host_capi.cpp"),

@@ -78,4 +78,13 @@ __device__ __forceinline__ uint64_t sat_u64(double f, double maxv_as_double, uin
     return (uint64_t)f;
 }
 
+// write_color's byte (color.rs:8-28): linear_to_gamma (sqrt of a positive value, else 0;
+// NaN -> 0), INTENSITY.clamp to [0, 0.999], then `(256.0 * c) as i32`.
+__device__ __forceinline__ uint8_t color_byte(double c) {
+    double g = c > 0.0 ? sqrt(c) : 0.0;
+    if (g < 0.000) g = 0.000;
+    if (g > 0.999) g = 0.999;
+    return (uint8_t)sat_i32(256.0 * g);
+}
+
 }  // namespace gsd

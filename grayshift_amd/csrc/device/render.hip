@@ -113,7 +113,8 @@ struct KParams {
     // pixel running the reference's batch loop (camera.rs:135-165) to completion.
     uint32_t chunk, cpp, n_items, pad2;
     double* partial;
-    float* out;
+    float* out;     // linear colour per packed pixel (nullable when out8 is set)
+    uint8_t* out8;  // write_color bytes of the f64 colour per packed pixel (nullable)
     unsigned long long* counters;
     uint32_t* queue;
     uint32_t* item_visits;  // diagnostic: node visits per packed pixel (nullable)
@@ -645,10 +646,19 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 if (!stop) stop = (uint32_t)sat_u64(scount, 4294967295.0, 4294967295ull) > P->ss.max_samples;
                 if (stop) {
                     const uint32_t item = LI(L_ITEM);
-                    float* o = P->out + (size_t)item * 3;
-                    o[0] = (float)(LD(L_CSR) / scount);
-                    o[1] = (float)(LD(L_CSG) / scount);
-                    o[2] = (float)(LD(L_CSB) / scount);
+                    const double cr = LD(L_CSR) / scount, cg = LD(L_CSG) / scount, cb = LD(L_CSB) / scount;
+                    if (P->out) {
+                        float* o = P->out + (size_t)item * 3;
+                        o[0] = (float)cr;
+                        o[1] = (float)cg;
+                        o[2] = (float)cb;
+                    }
+                    if (P->out8) {
+                        uint8_t* o8 = P->out8 + (size_t)item * 3;
+                        o8[0] = color_byte(cr);
+                        o8[1] = color_byte(cg);
+                        o8[2] = color_byte(cb);
+                    }
                     atomicAdd(&s_cnt[C_PIX], 1ull);
 #ifndef GS_STAMPS
                     if (P->item_visits) P->item_visits[item] = c_nodes;
@@ -742,10 +752,18 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     const uint32_t pj = (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + y;
                     if (pi >= (uint32_t)cam.image_width || pj >= (uint32_t)cam.image_height) {
                         if (!P->chunk) {  // padding pixel (chunked: gs_combine_kernel writes it)
-                            float* o = P->out + (size_t)item * 3;
-                            o[0] = 0.0f;
-                            o[1] = 0.0f;
-                            o[2] = 0.0f;
+                            if (P->out) {
+                                float* o = P->out + (size_t)item * 3;
+                                o[0] = 0.0f;
+                                o[1] = 0.0f;
+                                o[2] = 0.0f;
+                            }
+                            if (P->out8) {
+                                uint8_t* o8 = P->out8 + (size_t)item * 3;
+                                o8[0] = 0;
+                                o8[1] = 0;
+                                o8[2] = 0;
+                            }
                         }
                     } else {
                         LI(L_PIX) = pj * (uint32_t)cam.image_width + pi;
@@ -954,11 +972,19 @@ __global__ void gs_combine_kernel(const KParams* __restrict__ P) {
         const uint32_t tile = (uint32_t)P->rank + slot * (uint32_t)P->world_size;
         const uint32_t pi = (tile % (uint32_t)P->tiles_x) * (uint32_t)P->tile_w + w % (uint32_t)P->tile_w;
         const uint32_t pj = (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + w / (uint32_t)P->tile_w;
-        float* o = P->out + (size_t)k * 3;
+        float* o = P->out ? P->out + (size_t)k * 3 : nullptr;
+        uint8_t* o8 = P->out8 ? P->out8 + (size_t)k * 3 : nullptr;
         if (pi >= (uint32_t)P->cam.image_width || pj >= (uint32_t)P->cam.image_height) {
-            o[0] = 0.0f;
-            o[1] = 0.0f;
-            o[2] = 0.0f;
+            if (o) {
+                o[0] = 0.0f;
+                o[1] = 0.0f;
+                o[2] = 0.0f;
+            }
+            if (o8) {
+                o8[0] = 0;
+                o8[1] = 0;
+                o8[2] = 0;
+            }
             continue;
         }
         const double* p = P->partial + (size_t)k * cpp * 3;
@@ -968,9 +994,17 @@ __global__ void gs_combine_kernel(const KParams* __restrict__ P) {
             g += p[c * 3 + 1];
             b += p[c * 3 + 2];
         }
-        o[0] = (float)(r / scount);
-        o[1] = (float)(g / scount);
-        o[2] = (float)(b / scount);
+        const double cr = r / scount, cg = g / scount, cb = b / scount;
+        if (o) {
+            o[0] = (float)cr;
+            o[1] = (float)cg;
+            o[2] = (float)cb;
+        }
+        if (o8) {
+            o8[0] = color_byte(cr);
+            o8[1] = color_byte(cg);
+            o8[2] = color_byte(cb);
+        }
     }
 }
 
@@ -1383,13 +1417,23 @@ int64_t gs_partition_capacity(const gs_camera* cam, const gs_partition* p) {
 gs_status gs_render_tiles_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
                                 uint64_t seed, const gs_partition* part, float* d_out, gs_counters* d_counters,
                                 void* stream) {
-    return gs_render_tiles_debug_async(ds, cam, ss, seed, part, d_out, d_counters, nullptr, stream);
+    if (!d_out) return fail(GS_ERR_ARG, "null argument");
+    gs_render_outputs o{d_out, nullptr, nullptr};
+    return gs_render_tiles_ex_async(ds, cam, ss, seed, part, &o, d_counters, stream);
 }
 
 gs_status gs_render_tiles_debug_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
                                       uint64_t seed, const gs_partition* part, float* d_out,
                                       gs_counters* d_counters, uint32_t* d_item_visits, void* stream) {
-    if (!ds || !cam || !ss || !part || !d_out) return fail(GS_ERR_ARG, "null argument");
+    if (!d_out) return fail(GS_ERR_ARG, "null argument");
+    gs_render_outputs o{d_out, nullptr, d_item_visits};
+    return gs_render_tiles_ex_async(ds, cam, ss, seed, part, &o, d_counters, stream);
+}
+
+gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
+                                   uint64_t seed, const gs_partition* part, const gs_render_outputs* outs,
+                                   gs_counters* d_counters, void* stream) {
+    if (!ds || !cam || !ss || !part || !outs || (!outs->rgb && !outs->rgb8)) return fail(GS_ERR_ARG, "null argument");
     if (!part_ok(cam, part)) return fail(GS_ERR_ARG, "bad partition / image size");
     if (ss->batch_size == 0) return fail(GS_ERR_ARG, "batch_size 0 never terminates (camera.rs:137)");
     int64_t cap = gs_partition_capacity(cam, part);
@@ -1441,10 +1485,11 @@ gs_status gs_render_tiles_debug_async(const gs_device_scene* ds, const gs_camera
         }
         kp.partial = mds->partial;
     }
-    kp.out = d_out;
+    kp.out = outs->rgb;
+    kp.out8 = outs->rgb8;
     kp.counters = (unsigned long long*)d_counters;
     kp.queue = ds->queue;
-    kp.item_visits = d_item_visits;
+    kp.item_visits = outs->item_visits;
     KArgs a{};
     a.nodes = ds->dev.nodes;
     a.spheres = ds->dev.spheres;
@@ -1538,6 +1583,67 @@ gs_status gs_render(const gs_flat_scene* scene, const gs_camera* cam, const gs_s
         if (e == hipSuccess) e = hipMemcpy(out_rgb, d_frame, W * H * 12, hipMemcpyDeviceToHost);
         if (e == hipSuccess && counters) e = hipMemcpy(counters, d_cnt, sizeof(gs_counters), hipMemcpyDeviceToHost);
         if (e != hipSuccess) r = fail(GS_ERR_HIP, hipGetErrorString(e));
+    }
+    cleanup();
+    return r;
+}
+
+gs_status gs_render_ppm(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
+                        char* out_text, int64_t text_capacity, int64_t* out_len, gs_counters* counters) {
+    if (!scene || !cam || !ss || !out_text || !out_len) return fail(GS_ERR_ARG, "null argument");
+    const int64_t need = gs_ppm_max_bytes(cam->image_width, cam->image_height);
+    if (need < 0) return fail(GS_ERR_ARG, "bad image size");
+    if (text_capacity < need) return fail(GS_ERR_ARG, "text capacity below gs_ppm_max_bytes");
+    gs_device_scene* ds = nullptr;
+    gs_status r = gs_device_scene_create(scene, &ds);
+    if (r != GS_OK) return r;
+    gs_partition p{0, 1, 64, 64};
+    const int64_t cap = gs_partition_capacity(cam, &p);
+    const size_t W = (size_t)cam->image_width, H = (size_t)cam->image_height;
+    const int64_t scratch = gs_ppm_scratch_bytes(cam->image_width, cam->image_height);
+    uint8_t *d_pack = nullptr, *d_frame = nullptr;
+    char* d_text = nullptr;
+    void* d_scratch = nullptr;
+    int64_t* d_len = nullptr;
+    gs_counters* d_cnt = nullptr;
+    auto cleanup = [&]() {
+        if (d_pack) (void)hipFree(d_pack);
+        if (d_frame) (void)hipFree(d_frame);
+        if (d_text) (void)hipFree(d_text);
+        if (d_scratch) (void)hipFree(d_scratch);
+        if (d_len) (void)hipFree(d_len);
+        if (d_cnt) (void)hipFree(d_cnt);
+        gs_device_scene_destroy(ds);
+    };
+    if (hipMalloc(&d_pack, (size_t)cap * 3 + 16) != hipSuccess || hipMalloc(&d_frame, W * H * 3 + 16) != hipSuccess ||
+        hipMalloc(&d_text, (size_t)need) != hipSuccess || hipMalloc(&d_scratch, (size_t)scratch) != hipSuccess ||
+        hipMalloc(&d_len, 8) != hipSuccess || hipMalloc(&d_cnt, sizeof(gs_counters)) != hipSuccess) {
+        cleanup();
+        return fail(GS_ERR_OOM, "hipMalloc failed");
+    }
+    hipError_t e = hipMemset(d_cnt, 0, sizeof(gs_counters));
+    if (e != hipSuccess) {
+        cleanup();
+        return fail(GS_ERR_HIP, hipGetErrorString(e));
+    }
+    gs_render_outputs o{nullptr, d_pack, nullptr};
+    r = gs_render_tiles_ex_async(ds, cam, ss, seed, &p, &o, d_cnt, nullptr);
+    if (r == GS_OK) r = gs_unpack_tiles_u8_async(cam, 1, p.tile_w, p.tile_h, cap, d_pack, d_frame, nullptr);
+    if (r == GS_OK)
+        r = gs_ppm_encode_async(d_frame, cam->image_width, cam->image_height, d_text, need, d_len, d_scratch, scratch,
+                                nullptr);
+    if (r == GS_OK) {
+        int64_t len = 0;
+        e = hipDeviceSynchronize();
+        if (e == hipSuccess) e = hipMemcpy(&len, d_len, 8, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && (len <= 0 || len > need)) {
+            cleanup();
+            return fail(GS_ERR_HIP, "PPM encoder returned a bad length");
+        }
+        if (e == hipSuccess) e = hipMemcpy(out_text, d_text, (size_t)len, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && counters) e = hipMemcpy(counters, d_cnt, sizeof(gs_counters), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) r = fail(GS_ERR_HIP, hipGetErrorString(e));
+        else *out_len = len;
     }
     cleanup();
     return r;

@@ -1,6 +1,6 @@
 // camera.cpp — Camera::new (camera.rs:39-98) and Camera::render (camera.rs:100-121).
-// render() keeps the reference's output stage on the host (PPM header + write_color)
-// and replaces the rayon pixel loop (camera.rs:105-114) with one gs_render call.
+// render() replaces the rayon pixel loop (camera.rs:105-114) and the output stage
+// (:101-103,116-118) with one gs_render_ppm call: bytes and text come from the device.
 #include <cstring>
 #include <sstream>
 
@@ -56,10 +56,23 @@ void Camera::render_linear(const Hittable& world, float* out_rgb, gs_counters* c
     check(gs_render(&fs->view, &cam, &ss, seed, out_rgb, counters));
 }
 
+std::string Camera::render_ppm(const Hittable& world, gs_counters* counters, uint64_t seed) const {
+    auto fs = flatten_world(world, bg);
+    const int64_t cap = gs_ppm_max_bytes(cam.image_width, cam.image_height);
+    if (cap < 0) throw std::runtime_error("bad image size");
+    std::string text((size_t)cap, '\0');
+    int64_t len = 0;
+    check(gs_render_ppm(&fs->view, &cam, &ss, seed, &text[0], cap, &len, counters));
+    text.resize((size_t)len);
+    return text;
+}
+
+// The whole of camera.rs:100-121: the PPM text (header, then write_color per pixel of
+// the f64 colour) is formatted on the device and written here with one call.
 void Camera::render(const Hittable& world, std::ostream& image_file, uint64_t seed) const {
-    std::vector<float> rgb((size_t)cam.image_width * (size_t)cam.image_height * 3);
-    render_linear(world, rgb.data(), nullptr, seed);
-    write_ppm(image_file, cam.image_width, cam.image_height, rgb.data());
+    const std::string text = render_ppm(world, nullptr, seed);
+    image_file.write(text.data(), (std::streamsize)text.size());
+    if (!image_file) throw std::runtime_error("PPM write failed");
 }
 
 int32_t color_byte(double c) {  // color.rs:8-28

@@ -207,6 +207,23 @@ gs_status gs_host_render_spec(const gs_scene_spec* spec, const gs_camera_spec* c
     });
 }
 
+gs_status gs_host_render_ppm_spec(const gs_scene_spec* spec, const gs_camera_spec* c, const gs_sample_settings* ss,
+                                  uint64_t seed, char* out_text, int64_t text_capacity, int64_t* out_len,
+                                  gs_counters* counters) {
+    if (!spec || !c || !ss || !out_text || !out_len) return fail(GS_ERR_ARG, "null argument");
+    return guarded([&]() {
+        SpecBuilder b(*spec);
+        auto world = b.world();
+        Camera cam(c->aspect_ratio, c->image_width, SampleSettings{ss->confidence, ss->tolerance, ss->batch_size, ss->max_samples},
+                   c->max_depth, c->v_fov, Vec3(c->look_from[0], c->look_from[1], c->look_from[2]),
+                   Vec3(c->look_at[0], c->look_at[1], c->look_at[2]), Vec3(c->vup[0], c->vup[1], c->vup[2]),
+                   c->defocus_angle, c->focus_distance, b.background());
+        auto fs = flatten_world(*world, cam.background());
+        return gs_render_ppm(&fs->view, &cam.fields(), &cam.settings(), seed, out_text, text_capacity, out_len,
+                             counters);
+    });
+}
+
 gs_status gs_host_write_ppm(const char* path, int32_t width, int32_t height, const float* rgb) {
     if (!path || !rgb || width <= 0 || height <= 0) return fail(GS_ERR_ARG, "bad argument");
     return guarded([&]() {

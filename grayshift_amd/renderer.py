@@ -29,6 +29,27 @@ def render(scene, seed=1):
     return out, cnt.as_dict()
 
 
+def render_ppm(scene, seed=1):
+    """The whole of Camera::render (camera.rs:100-121): returns (PPM text as bytes, counters).
+    Pixel bytes (write_color of the f64 colour) and the text are produced on the device."""
+    cam = camera(scene.camera)
+    cap = N.lib.gs_ppm_max_bytes(cam.image_width, cam.image_height)
+    if cap < 0:
+        raise ValueError("bad image size")
+    buf = C.create_string_buffer(int(cap))
+    n = C.c_int64()
+    cnt = N.gs_counters()
+    N.check(N.lib.gs_host_render_ppm_spec(scene.spec.ptr(), C.byref(scene.camera), C.byref(scene.settings), seed,
+                                          buf, cap, C.byref(n), C.byref(cnt)))
+    return buf.raw[:n.value], cnt.as_dict()
+
+
+def ppm_encode_async(d_rgb8, width, height, d_text, text_capacity, d_len, d_scratch, scratch_bytes, stream=0):
+    """Format a device W*H*3 byte frame as the reference's PPM text on the device."""
+    N.check(N.lib.gs_ppm_encode_async(C.c_void_p(d_rgb8), width, height, C.c_void_p(d_text), text_capacity,
+                                      C.c_void_p(d_len), C.c_void_p(d_scratch), scratch_bytes, C.c_void_p(stream)))
+
+
 def set_tuning(shade_batch=52, blocks_per_cu=0, leaf_batch=8, sample_chunk=-1):
     """Process-wide launch tuning (see gs_set_tuning in include/grayshift_gpu.h)."""
     N.check(N.lib.gs_set_tuning(shade_batch, blocks_per_cu, leaf_batch, sample_chunk))
@@ -94,6 +115,18 @@ class Renderer:
         N.check(N.lib.gs_render_tiles_async(self.dev, C.byref(self.cam), C.byref(self.settings), seed,
                                             C.byref(self.part), C.c_void_p(d_packed), C.c_void_p(d_counters),
                                             C.c_void_p(stream)))
+
+    def render_ex_async(self, d_rgb=0, d_rgb8=0, d_counters=0, stream=0, seed=1, d_item_visits=0):
+        """Either or both outputs: d_rgb capacity*3 f32, d_rgb8 capacity*3 u8 (write_color bytes)."""
+        o = N.gs_render_outputs(d_rgb or None, d_rgb8 or None, d_item_visits or None)
+        N.check(N.lib.gs_render_tiles_ex_async(self.dev, C.byref(self.cam), C.byref(self.settings), seed,
+                                               C.byref(self.part), C.byref(o), C.c_void_p(d_counters),
+                                               C.c_void_p(stream)))
+
+    def unpack_u8_async(self, d_gathered, d_frame, world_size, stream=0):
+        N.check(N.lib.gs_unpack_tiles_u8_async(C.byref(self.cam), world_size, self.part.tile_w, self.part.tile_h,
+                                               self.capacity, C.c_void_p(d_gathered), C.c_void_p(d_frame),
+                                               C.c_void_p(stream)))
 
     def unpack_async(self, d_gathered, d_frame, world_size, stream=0):
         N.check(N.lib.gs_unpack_tiles_async(C.byref(self.cam), world_size, self.part.tile_w, self.part.tile_h,

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 2
+#define GS_ABI_VERSION 3
 
 typedef int32_t gs_status;
 enum {
@@ -227,6 +227,21 @@ gs_status gs_render_tiles_async(const gs_device_scene* scene, const gs_camera* c
                                 const gs_partition* part, float* d_packed_rgb,
                                 gs_counters* d_counters, void* stream);
 
+/* Outputs of one launch, per packed pixel (capacity entries; padding pixels get 0).
+ * At least one of rgb / rgb8 must be set. */
+typedef struct gs_render_outputs {
+    float* rgb;            /* capacity*3 f32, linear colour (camera.rs:167), nullable */
+    uint8_t* rgb8;         /* capacity*3 u8, write_color's bytes (color.rs:8-18) of the f64
+                              colour (not of the f32 one), nullable */
+    uint32_t* item_visits; /* capacity u32, BVH node visits per pixel (diagnostic), nullable */
+} gs_render_outputs;
+
+/* gs_render_tiles_async with a choice of outputs (ABI 3). */
+gs_status gs_render_tiles_ex_async(const gs_device_scene* scene, const gs_camera* cam,
+                                   const gs_sample_settings* ss, uint64_t seed,
+                                   const gs_partition* part, const gs_render_outputs* out,
+                                   gs_counters* d_counters, void* stream);
+
 /* Diagnostic variant: also writes, per packed pixel, the number of BVH node visits
  * its samples made (d_item_visits: capacity u32, nullable). */
 gs_status gs_render_tiles_debug_async(const gs_device_scene* scene, const gs_camera* cam,
@@ -239,6 +254,33 @@ gs_status gs_render_tiles_debug_async(const gs_device_scene* scene, const gs_cam
 gs_status gs_unpack_tiles_async(const gs_camera* cam, int32_t world_size, int32_t tile_w,
                                 int32_t tile_h, int64_t capacity, const float* d_gathered,
                                 float* d_frame, void* stream);
+
+/* As gs_unpack_tiles_async, for the 3-byte rgb8 output (ABI 3). */
+gs_status gs_unpack_tiles_u8_async(const gs_camera* cam, int32_t world_size, int32_t tile_w,
+                                   int32_t tile_h, int64_t capacity, const uint8_t* d_gathered,
+                                   uint8_t* d_frame, void* stream);
+
+/* ---- Output stage on the device (camera.rs:101-103,116-118; color.rs:8-18) (ABI 3) ----
+ * The reference writes an ASCII PPM: "P3\n{W} {H}\n255\n", then one "{r} {g} {b}\n"
+ * line per pixel in row-major order.  gs_ppm_encode_async formats that text on the
+ * device from a W*H*3 byte frame (rgb8 output, unpacked), in one pass: each block
+ * formats 2048 pixels in LDS and finds its output offset by a decoupled look-back over
+ * its predecessors' lengths.  The host writes the result with one write call. */
+int64_t gs_ppm_max_bytes(int32_t width, int32_t height);     /* text capacity bound */
+int64_t gs_ppm_scratch_bytes(int32_t width, int32_t height); /* device scratch size */
+/* d_rgb8: device, W*H*3 bytes; d_text: device, >= gs_ppm_max_bytes; d_len: device
+ * int64, receives the text length; d_scratch: device, >= gs_ppm_scratch_bytes (its
+ * contents are overwritten; it may be reused after the stream has passed this call). */
+gs_status gs_ppm_encode_async(const uint8_t* d_rgb8, int32_t width, int32_t height, char* d_text,
+                              int64_t text_capacity, int64_t* d_len, void* d_scratch,
+                              int64_t scratch_bytes, void* stream);
+
+/* Synchronous full render to PPM text on the current device: the whole of
+ * Camera::render (camera.rs:100-121) past the world build.  out_text: host buffer of
+ * text_capacity >= gs_ppm_max_bytes(W, H) bytes; *out_len receives the length. */
+gs_status gs_render_ppm(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss,
+                        uint64_t seed, char* out_text, int64_t text_capacity, int64_t* out_len,
+                        gs_counters* counters);
 
 /* Synchronous full-frame render on the current device: upload, render, copy back.
  * out_rgb: host buffer W*H*3 f32 (linear).  counters: host, nullable.  This is the

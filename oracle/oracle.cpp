@@ -974,12 +974,15 @@ extern "C" {
 
 const char* oracle_last_error(void) { return tl_err.c_str(); }
 
+int32_t oracle_color_byte(double c);
+
 /* Render pixels of the frame (all, or the listed subset) into out_rgb
- * (n_pixels*3 f32, in subset order, or the full W*H*3 frame).
+ * (n_pixels*3 f32, in subset order, or the full W*H*3 frame), and, when out_rgb8 is
+ * not NULL, write_color's bytes of the f64 colour in the same order.
  * Returns 0 on success, -1 on error (message in oracle_last_error). */
 int oracle_render(const gs_scene_spec* spec, const gs_camera_spec* cam, const gs_sample_settings* ss,
                   uint64_t seed, int32_t n_threads, const int32_t* subset, int64_t n_subset,
-                  float* out_rgb, gs_counters* counters) {
+                  float* out_rgb, gs_counters* counters, uint8_t* out_rgb8) {
     try {
         World w;
         build_world(*spec, w);
@@ -1006,6 +1009,11 @@ int oracle_render(const gs_scene_spec* spec, const gs_camera_spec* cam, const gs
                             out_rgb[k * 3 + 0] = (float)c.x;
                             out_rgb[k * 3 + 1] = (float)c.y;
                             out_rgb[k * 3 + 2] = (float)c.z;
+                            if (out_rgb8) { /* write_color (color.rs:8-18) of the f64 colour */
+                                out_rgb8[k * 3 + 0] = (uint8_t)oracle_color_byte(c.x);
+                                out_rgb8[k * 3 + 1] = (uint8_t)oracle_color_byte(c.y);
+                                out_rgb8[k * 3 + 2] = (uint8_t)oracle_color_byte(c.z);
+                            }
                         }
                     }
                     per[t] = tl_cnt;
@@ -1097,6 +1105,17 @@ int32_t oracle_color_byte(double c) {
     double g = c > 0.0 ? std::sqrt(c) : 0.0;
     double cl = Interval(0.0, 0.999).clamp(g);
     return sat_i32(256.0 * cl);
+}
+/* Camera::render's text (camera.rs:101-103,116-118; color.rs:17 `writeln!` of
+ * "{r} {g} {b}") from a W*H*3 byte frame.  Returns the length, or the length needed
+ * when out is NULL / too small. */
+int64_t oracle_ppm_text(const uint8_t* rgb8, int32_t w, int32_t h, char* out, int64_t cap) {
+    std::string t = "P3\n" + std::to_string(w) + " " + std::to_string(h) + "\n255\n";
+    const int64_t n = (int64_t)w * h;
+    for (int64_t k = 0; k < n; k++)
+        t += std::to_string(rgb8[3 * k]) + " " + std::to_string(rgb8[3 * k + 1]) + " " + std::to_string(rgb8[3 * k + 2]) + "\n";
+    if (out && cap >= (int64_t)t.size()) std::memcpy(out, t.data(), t.size());
+    return (int64_t)t.size();
 }
 /* Checkered texture parity (texture.rs:58-70): returns 1 for even. */
 int oracle_checker_even(double scale, const double* p) {

@@ -27,7 +27,9 @@ def lib():
         L.oracle_render.restype = C.c_int
         L.oracle_render.argtypes = [C.POINTER(N.gs_scene_spec), C.POINTER(N.gs_camera_spec),
                                     C.POINTER(N.gs_sample_settings), C.c_uint64, C.c_int32, P, C.c_int64, P,
-                                    C.POINTER(N.gs_counters)]
+                                    C.POINTER(N.gs_counters), P]
+        L.oracle_ppm_text.restype = C.c_int64
+        L.oracle_ppm_text.argtypes = [P, C.c_int32, C.c_int32, P, C.c_int64]
         L.oracle_camera_fields.argtypes = [C.POINTER(N.gs_camera_spec), P]
         L.oracle_stream_seed.restype = C.c_uint64
         L.oracle_stream_seed.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32]
@@ -56,8 +58,9 @@ def _d(a):
     return a, a.ctypes.data
 
 
-def render(scene, seed=1, threads=0, subset=None):
-    """Render `scene` (scenes.Scene) on the CPU.  Returns (rgb f32 [n,3] or [H,W,3], counters dict)."""
+def render(scene, seed=1, threads=0, subset=None, bytes_out=False):
+    """Render `scene` (scenes.Scene) on the CPU.  Returns (rgb f32 [n,3] or [H,W,3], counters dict),
+    plus write_color's bytes of the f64 colour (u8, same shape) when bytes_out."""
     from grayshift_amd import _native as N
     L = lib()
     if not threads:  # the GPU box's CPU share is 16 cores; nproc reports the whole machine
@@ -66,15 +69,35 @@ def render(scene, seed=1, threads=0, subset=None):
     if subset is not None:
         sub = np.ascontiguousarray(subset, dtype=np.int32)
         out = np.zeros((len(sub), 3), dtype=np.float32)
-        r = L.oracle_render(scene.spec.ptr(), C.byref(scene.camera), C.byref(scene.settings), seed, threads,
-                            sub.ctypes.data, len(sub), out.ctypes.data, C.byref(cnt))
+        sub_ptr, n_sub = sub.ctypes.data, len(sub)
     else:
         out = np.zeros((scene.height, scene.width, 3), dtype=np.float32)
-        r = L.oracle_render(scene.spec.ptr(), C.byref(scene.camera), C.byref(scene.settings), seed, threads,
-                            None, 0, out.ctypes.data, C.byref(cnt))
+        sub_ptr, n_sub = None, 0
+    b8 = np.zeros(out.shape, dtype=np.uint8) if bytes_out else None
+    r = L.oracle_render(scene.spec.ptr(), C.byref(scene.camera), C.byref(scene.settings), seed, threads,
+                        sub_ptr, n_sub, out.ctypes.data, C.byref(cnt), b8.ctypes.data if bytes_out else None)
     if r != 0:
         raise RuntimeError("oracle: " + L.oracle_last_error().decode())
+    if bytes_out:
+        return out, cnt.as_dict(), b8
     return out, cnt.as_dict()
+
+
+def ppm_text(rgb8):
+    """Camera::render's PPM text (camera.rs:101-103,116-118) for an [H,W,3] byte frame."""
+    a = np.ascontiguousarray(rgb8, dtype=np.uint8)
+    h, w = a.shape[0], a.shape[1]
+    L = lib()
+    n = L.oracle_ppm_text(a.ctypes.data, w, h, None, 0)
+    buf = C.create_string_buffer(int(n))
+    L.oracle_ppm_text(a.ctypes.data, w, h, buf, n)
+    return buf.raw[:n]
+
+
+def render_ppm(scene, seed=1, threads=0):
+    """The oracle's Camera::render output: (PPM bytes, counters)."""
+    _, cnt, b8 = render(scene, seed=seed, threads=threads, bytes_out=True)
+    return ppm_text(b8), cnt
 
 
 def bvh_topology(spec):

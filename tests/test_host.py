@@ -39,7 +39,7 @@ def test_every_declared_symbol_is_exported(built):
 
 
 def test_version_and_error_channel():
-    assert N.lib.gs_version() == N.GS_ABI_VERSION == 2
+    assert N.lib.gs_version() == N.GS_ABI_VERSION == 3
     assert N.lib.gs_set_tuning(0, 0, 0, -1) == N.GS_ERR_ARG
     assert b"tuning" in N.lib.gs_last_error()
     assert N.lib.gs_set_tuning(60, 0, 0, -1) == N.GS_OK
@@ -225,3 +225,51 @@ def test_no_cpu_fallback_without_device():
     env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     assert "ERR" in r.stdout, r.stdout + r.stderr
+
+
+# ------------------------------------------------- output stage (PPM text)
+def _ppm_reference_text(b8):
+    """camera.rs:101-103 header, then color.rs:17 `writeln!("{r} {g} {b}")` per pixel."""
+    h, w = b8.shape[0], b8.shape[1]
+    lines = ["P3", "%d %d" % (w, h), "255"] + ["%d %d %d" % tuple(p) for p in b8.reshape(-1, 3)]
+    return ("\n".join(lines) + "\n").encode()
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (2, 1), (7, 3), (64, 32)])
+def test_oracle_ppm_text_format(w, h):
+    rng = np.random.default_rng(w * 100 + h)
+    b8 = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
+    b8.flat[:4] = [0, 9, 10, 255][:min(4, b8.size)]
+    assert oracle.ppm_text(b8) == _ppm_reference_text(b8)
+
+
+def test_oracle_bytes_are_write_color_of_the_f64_colour():
+    sc = _scene("C3")
+    sc = type(sc)(sc.name, sc.spec, g.camera_spec(1.0, 12, 20, 40.0, (278.0, 278.0, -800.0), (278.0, 278.0, 0.0),
+                                                  (0.0, 1.0, 0.0), 0.0, 10.0), g.fixed_spp(2))
+    rgb, _, b8 = oracle.render(sc, seed=4, bytes_out=True)
+    # bytes come from the f64 colour: equal to the f32 frame's bytes except where the
+    # f32 rounding crosses a quantisation step (rare); every byte is write_color's range
+    f32_bytes = np.vectorize(oracle.color_byte)(rgb.astype(np.float64))
+    assert (np.abs(f32_bytes - b8.astype(np.int64)) <= 1).all()
+    assert (f32_bytes == b8).mean() > 0.99
+
+
+def test_ppm_sizes():
+    hdr = len(b"P3\n3840 2160\n255\n")
+    assert N.lib.gs_ppm_max_bytes(3840, 2160) == hdr + 3840 * 2160 * 12
+    assert N.lib.gs_ppm_max_bytes(0, 5) == -1 and N.lib.gs_ppm_scratch_bytes(5, -1) == -1
+    assert N.lib.gs_ppm_scratch_bytes(1, 1) == 64 + 8
+    assert N.lib.gs_ppm_scratch_bytes(2048, 1) == 64 + 8 and N.lib.gs_ppm_scratch_bytes(2049, 1) == 64 + 16
+
+
+def test_ppm_encode_rejects_bad_arguments_before_the_device():
+    P = C.c_void_p
+    ok = P(0x1000)
+    assert N.lib.gs_ppm_encode_async(None, 4, 4, ok, 1 << 20, ok, ok, 1 << 20, None) == N.GS_ERR_ARG
+    assert N.lib.gs_ppm_encode_async(ok, 0, 4, ok, 1 << 20, ok, ok, 1 << 20, None) == N.GS_ERR_ARG
+    assert N.lib.gs_ppm_encode_async(ok, 4, 4, ok, 10, ok, ok, 1 << 20, None) == N.GS_ERR_ARG
+    assert b"capacity" in N.lib.gs_last_error()
+    assert N.lib.gs_ppm_encode_async(ok, 4, 4, ok, 1 << 20, ok, ok, 8, None) == N.GS_ERR_ARG
+    assert N.lib.gs_ppm_encode_async(P(0x1001), 4, 4, ok, 1 << 20, ok, ok, 1 << 20, None) == N.GS_ERR_ARG
+    assert b"aligned" in N.lib.gs_last_error()
