@@ -8,10 +8,12 @@
 //     "P3\n{W} {H}\n255\n"  then  "{r} {g} {b}\n"  per pixel, row-major
 //
 // Byte work, HBM-bound (no arithmetic to speak of): 3 B read and 6..12 B written per
-// pixel.  One pass: a block formats 2048 pixels in LDS, learns where its text starts by a
-// decoupled look-back over its predecessors' lengths (one 8-byte {flag, length} granule
-// per block, written and polled with agent-scope atomics, so the hand-off is coherent
-// across the 8 XCDs' L2s), then streams its text out with aligned dword stores.
+// pixel.  Three launches on the stream, no inter-block waiting: (1) each block of 2048
+// pixels sizes its text; (2) one block scans the block lengths into offsets; (3) each
+// block formats its text in LDS at the destination's alignment and streams it out in
+// 16-byte stores.  (A one-pass decoupled look-back was measured slower here: with every
+// block resident at once, only the first blocks hold inclusive prefixes and the walk is
+// a chain of cross-XCD load round trips; 87 µs vs this at 4K, see DESIGN.md.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,9 +31,7 @@ constexpr int PPM_THREADS = 256;
 constexpr int PPM_PX_PER_THREAD = 8;
 constexpr int PPM_PX = PPM_THREADS * PPM_PX_PER_THREAD;  // pixels per block
 constexpr int PPM_MAX_LINE = 12;                          // "255 255 255\n"
-constexpr uint64_t ST_AGG = 1ull << 62;                   // block's own length is known
-constexpr uint64_t ST_INC = 2ull << 62;                   // inclusive prefix is known
-constexpr uint64_t ST_VAL = (1ull << 62) - 1;
+constexpr int SCAN_THREADS = 1024;
 
 struct PpmHeader {
     char c[40];
@@ -56,26 +56,18 @@ __device__ __forceinline__ uint32_t put_u8(uint8_t* o, uint32_t v) {
     return 1;
 }
 
-__global__ __launch_bounds__(PPM_THREADS) void gs_ppm_kernel(const uint8_t* __restrict__ in, uint64_t n_px,
-                                                             char* __restrict__ out, int64_t* __restrict__ len_out,
-                                                             unsigned long long* __restrict__ status,
-                                                             uint32_t* __restrict__ ticket, uint32_t n_blocks,
-                                                             PpmHeader hdr) {
-    __shared__ uint32_t s_in[PPM_PX * 3 / 4];
-    __shared__ uint8_t s_out[PPM_PX * PPM_MAX_LINE];
-    __shared__ uint32_t s_wave[PPM_THREADS / 64];
-    __shared__ uint32_t s_bid;
-    __shared__ unsigned long long s_base;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    // Dynamic block ids in launch order: a block only ever waits on blocks that already run.
-    if (tid == 0) s_bid = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const uint32_t bid = s_bid;
-    const uint64_t px0 = (uint64_t)bid * PPM_PX;
-    const uint32_t npx = (uint32_t)((n_px - px0) < (uint64_t)PPM_PX ? (n_px - px0) : (uint64_t)PPM_PX);
-    const uint32_t nbytes = npx * 3u;
-
-    // Stage the block's input bytes (coalesced dwords; the host checked 4-byte alignment).
+// A block's pixels: stage their bytes in LDS (coalesced dwords; the host checked 4-byte
+// alignment), then each thread sizes the lines of its PPM_PX_PER_THREAD pixels.
+struct BlockPixels {
+    uint32_t npx, cnt, p_first, mine;
+};
+__device__ __forceinline__ BlockPixels stage_and_size(const uint8_t* __restrict__ in, uint64_t n_px, uint32_t blk,
+                                                      uint32_t* s_in) {
+    const uint32_t tid = threadIdx.x;
+    BlockPixels b;
+    const uint64_t px0 = (uint64_t)blk * PPM_PX;
+    b.npx = (uint32_t)((n_px - px0) < (uint64_t)PPM_PX ? (n_px - px0) : (uint64_t)PPM_PX);
+    const uint32_t nbytes = b.npx * 3u;
     const uint8_t* src = in + px0 * 3u;
     const uint32_t nfull = nbytes >> 2;
     for (uint32_t i = tid; i < nfull; i += PPM_THREADS) s_in[i] = reinterpret_cast<const uint32_t*>(src)[i];
@@ -86,36 +78,90 @@ __global__ __launch_bounds__(PPM_THREADS) void gs_ppm_kernel(const uint8_t* __re
     }
     __syncthreads();
     const uint8_t* sb = reinterpret_cast<const uint8_t*>(s_in);
-
-    // This thread's pixels and their text length.
-    const uint32_t p_first = tid * PPM_PX_PER_THREAD;
-    const uint32_t cnt = p_first >= npx ? 0u : (npx - p_first < PPM_PX_PER_THREAD ? npx - p_first : PPM_PX_PER_THREAD);
-    uint32_t mine = 0;
-    for (uint32_t k = 0; k < cnt; k++) {
-        const uint8_t* p = sb + (p_first + k) * 3u;
-        mine += digits(p[0]) + digits(p[1]) + digits(p[2]) + 3u;
+    b.p_first = tid * PPM_PX_PER_THREAD;
+    b.cnt = b.p_first >= b.npx ? 0u : (b.npx - b.p_first < PPM_PX_PER_THREAD ? b.npx - b.p_first : PPM_PX_PER_THREAD);
+    b.mine = 0;
+    for (uint32_t k = 0; k < b.cnt; k++) {
+        const uint8_t* p = sb + (b.p_first + k) * 3u;
+        b.mine += digits(p[0]) + digits(p[1]) + digits(p[2]) + 3u;
     }
-    // Block exclusive scan of the lengths: wave64 shuffles, then across the 4 waves.
-    uint32_t incl = mine;
+    return b;
+}
+
+// Block-wide exclusive scan (wave64 shuffles, then across the waves); returns the
+// thread's exclusive prefix, *total the block sum.  T: u32 or u64.
+template <typename T, int THREADS>
+__device__ __forceinline__ T block_scan(T mine, T* s_wave, T* total) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    T incl = mine;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t v = __shfl_up(incl, d, 64);
+        const T v = __shfl_up(incl, d, 64);
         if ((int)lane >= d) incl += v;
     }
     if (lane == 63) s_wave[wave] = incl;
     __syncthreads();
-    uint32_t wave_base = 0, total = 0;
+    T wave_base = 0, tot = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < PPM_THREADS / 64; w++) {
-        const uint32_t v = s_wave[w];
+    for (uint32_t w = 0; w < THREADS / 64; w++) {
+        const T v = s_wave[w];
         if (w < wave) wave_base += v;
-        total += v;
+        tot += v;
     }
-    uint32_t at = wave_base + incl - mine;
+    *total = tot;
+    return wave_base + incl - mine;
+}
 
-    // Format into LDS.
-    for (uint32_t k = 0; k < cnt; k++) {
-        const uint8_t* p = sb + (p_first + k) * 3u;
+// Pass 1: text length of each block's 2048 pixels.
+__global__ __launch_bounds__(PPM_THREADS) void gs_ppm_size_kernel(const uint8_t* __restrict__ in, uint64_t n_px,
+                                                                  uint64_t* __restrict__ blk_len) {
+    __shared__ uint32_t s_in[PPM_PX * 3 / 4];
+    __shared__ uint32_t s_wave[PPM_THREADS / 64];
+    const BlockPixels b = stage_and_size(in, n_px, blockIdx.x, s_in);
+    uint32_t total;
+    block_scan<uint32_t, PPM_THREADS>(b.mine, s_wave, &total);
+    if (threadIdx.x == 0) blk_len[blockIdx.x] = total;
+}
+
+// Pass 2 (one block): exclusive scan of the block lengths after the header, in place;
+// the header text and the total length.
+__global__ __launch_bounds__(SCAN_THREADS) void gs_ppm_scan_kernel(uint64_t* __restrict__ blk, uint32_t n_blocks,
+                                                                   char* __restrict__ out, int64_t* __restrict__ len_out,
+                                                                   PpmHeader hdr) {
+    __shared__ uint64_t s_wave[SCAN_THREADS / 64];
+    const uint32_t per = (n_blocks + SCAN_THREADS - 1) / SCAN_THREADS;
+    const uint32_t lo = threadIdx.x * per, hi = lo + per < n_blocks ? lo + per : n_blocks;
+    uint64_t mine = 0;
+    for (uint32_t i = lo; i < hi; i++) mine += blk[i];
+    uint64_t total;
+    uint64_t run = (uint64_t)hdr.len + block_scan<uint64_t, SCAN_THREADS>(mine, s_wave, &total);
+    for (uint32_t i = lo; i < hi; i++) {
+        const uint64_t v = blk[i];
+        blk[i] = run;
+        run += v;
+    }
+    if (threadIdx.x < (uint32_t)hdr.len) out[threadIdx.x] = hdr.c[threadIdx.x];
+    if (threadIdx.x == 0) *len_out = (int64_t)(hdr.len + total);
+}
+
+// Pass 3: format each block's text in LDS, shifted so that LDS offset and global address
+// agree modulo 16, and stream it out in 16-B stores (the two edge chunks, shared with the
+// neighbouring blocks, bytewise).
+__global__ __launch_bounds__(PPM_THREADS) void gs_ppm_kernel(const uint8_t* __restrict__ in, uint64_t n_px,
+                                                             const uint64_t* __restrict__ blk_off,
+                                                             char* __restrict__ out) {
+    __shared__ uint32_t s_in[PPM_PX * 3 / 4];
+    __shared__ __align__(16) uint8_t s_out[PPM_PX * PPM_MAX_LINE + 16];
+    __shared__ uint32_t s_wave[PPM_THREADS / 64];
+    const BlockPixels b = stage_and_size(in, n_px, blockIdx.x, s_in);
+    uint32_t total;
+    const uint32_t excl = block_scan<uint32_t, PPM_THREADS>(b.mine, s_wave, &total);
+    const uint64_t off = blk_off[blockIdx.x];
+    const uint32_t sh = (uint32_t)(off & 15u);
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(s_in);
+    uint32_t at = sh + excl;
+    for (uint32_t k = 0; k < b.cnt; k++) {
+        const uint8_t* p = sb + (b.p_first + k) * 3u;
         uint8_t* o = s_out + at;
         uint32_t n = put_u8(o, p[0]);
         o[n++] = ' ';
@@ -125,71 +171,60 @@ __global__ __launch_bounds__(PPM_THREADS) void gs_ppm_kernel(const uint8_t* __re
         o[n++] = '\n';
         at += n;
     }
-
-    // Decoupled look-back (one lane): publish this block's length, sum predecessors'
-    // lengths back to the first inclusive prefix, publish the inclusive prefix.
-    if (tid == 0) {
-        uint64_t base;
-        if (bid == 0) {
-            base = (uint64_t)hdr.len;
-        } else {
-            __hip_atomic_store(&status[bid], ST_AGG | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            base = 0;
-            uint32_t p = bid - 1;
-            for (;;) {
-                const uint64_t s = __hip_atomic_load(&status[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((s & ~ST_VAL) == 0) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                base += s & ST_VAL;
-                if ((s & ~ST_VAL) == ST_INC) break;
-                p--;  // block 0 always publishes ST_INC, so p never wraps
-            }
-        }
-        __hip_atomic_store(&status[bid], ST_INC | (base + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (bid == n_blocks - 1) *len_out = (int64_t)(base + total);
-        s_base = base;
-    }
-    if (bid == 0 && tid < (uint32_t)hdr.len) out[tid] = hdr.c[tid];
     __syncthreads();
-
-    // Stream the block's text out: byte head up to a dword boundary, dwords, byte tail.
-    const uint64_t off = s_base;
-    char* dst = out + off;
-    const uint32_t head = (uint32_t)((4u - (off & 3u)) & 3u) < total ? (uint32_t)((4u - (off & 3u)) & 3u) : total;
-    if (tid < head) dst[tid] = (char)s_out[tid];
-    const uint32_t nd = (total - head) >> 2;
-    uint32_t* dst32 = reinterpret_cast<uint32_t*>(dst + head);
-    for (uint32_t i = tid; i < nd; i += PPM_THREADS) {
-        const uint8_t* q = s_out + head + i * 4u;
-        dst32[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-    }
-    const uint32_t tail = (total - head) & 3u;
-    if (tid < tail) dst[head + nd * 4u + tid] = (char)s_out[head + nd * 4u + tid];
-}
-
-// Scatter rank-packed byte tiles into the frame (the rgb8 twin of gs_unpack_kernel).
-__global__ void gs_unpack_u8_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ frame, int32_t W,
-                                    int32_t H, int32_t world, int32_t tile_w, int32_t tile_h, int32_t tiles_x,
-                                    uint64_t capacity) {
-    const uint64_t total = capacity * (uint64_t)world;
-    const uint32_t tile_px = (uint32_t)(tile_w * tile_h);
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total; g += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t r = (uint32_t)(g / capacity);
-        const uint64_t k = g % capacity;
-        const uint32_t slot = (uint32_t)(k / tile_px), w = (uint32_t)(k % tile_px);
-        const uint32_t tile = r + slot * (uint32_t)world;
-        const int32_t x = (int32_t)((tile % (uint32_t)tiles_x) * (uint32_t)tile_w + w % (uint32_t)tile_w);
-        const int32_t y = (int32_t)((tile / (uint32_t)tiles_x) * (uint32_t)tile_h + w / (uint32_t)tile_w);
-        if (x < W && y < H) {
-            const size_t o = ((size_t)y * (size_t)W + (size_t)x) * 3;
-            frame[o] = in[g * 3];
-            frame[o + 1] = in[g * 3 + 1];
-            frame[o + 2] = in[g * 3 + 2];
+    char* base16 = out + (off - sh);
+    const uint32_t end = sh + total;
+    const uint32_t nchunks = (end + 15u) >> 4;
+    for (uint32_t c = threadIdx.x; c < nchunks; c += PPM_THREADS) {
+        const uint32_t lo = c * 16u, hi = lo + 16u;
+        if (lo >= sh && hi <= end) {
+            *reinterpret_cast<uint4*>(base16 + lo) = *reinterpret_cast<const uint4*>(s_out + lo);
+        } else {
+            for (uint32_t i = (lo < sh ? sh : lo); i < (hi < end ? hi : end); i++) base16[i] = (char)s_out[i];
         }
     }
 }
+
+// Scatter rank-packed tiles into the frame, for any per-pixel element of E bytes (12: f32
+// rgb, 3: u8 rgb).  A tile row is one contiguous run in both the packed buffer and the
+// frame, so whole V-byte vectors move at once whenever V divides the run, the frame row
+// and the tile's x offset (V = 16 for 1080p/4K with 64-px tiles); right-edge padding
+// pixels are whole vectors too under that condition, so a vector is stored or skipped.
+template <int V>
+struct VecOf;
+template <>
+struct VecOf<16> { using T = uint4; };
+template <>
+struct VecOf<4> { using T = uint32_t; };
+template <>
+struct VecOf<1> { using T = uint8_t; };
+
+template <int V>
+__global__ void gs_unpack_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ frame, uint32_t E, int32_t W,
+                                 int32_t H, int32_t world, int32_t tile_w, int32_t tile_h, int32_t tiles_x,
+                                 uint64_t capacity) {
+    using T = typename VecOf<V>::T;
+    const uint64_t run = (uint64_t)tile_w * E;  // bytes per tile row
+    const uint64_t rank_bytes = capacity * E;
+    const uint64_t units = rank_bytes * (uint64_t)world / V;
+    const uint64_t row_bytes = (uint64_t)W * E;
+    for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t b = u * V;
+        const uint32_t r = (uint32_t)(b / rank_bytes);
+        const uint64_t rb = b - (uint64_t)r * rank_bytes;
+        const uint64_t row = rb / run;  // slot * tile_h + ty
+        const uint64_t o = rb - row * run;
+        const uint32_t slot = (uint32_t)(row / (uint64_t)tile_h), ty = (uint32_t)(row % (uint64_t)tile_h);
+        const uint32_t tile = r + slot * (uint32_t)world;
+        const uint64_t x0b = (uint64_t)(tile % (uint32_t)tiles_x) * (uint64_t)tile_w * E;
+        const uint32_t y = (tile / (uint32_t)tiles_x) * (uint32_t)tile_h + ty;
+        if (y < (uint32_t)H && x0b + o < row_bytes)
+            *reinterpret_cast<T*>(frame + (uint64_t)y * row_bytes + x0b + o) = *reinterpret_cast<const T*>(in + b);
+    }
+}
+
+gs_status unpack(const gs_camera* cam, int32_t world_size, int32_t tile_w, int32_t tile_h, int64_t capacity,
+                 const void* d_in, void* d_frame, uint32_t E, void* stream);
 
 gs_status fail(gs_status code, const std::string& msg) {
     gs_set_last_error(msg.c_str());
@@ -209,6 +244,39 @@ uint32_t ppm_blocks(int32_t W, int32_t H) {
     return (uint32_t)((n + PPM_PX - 1) / PPM_PX);
 }
 
+gs_status unpack(const gs_camera* cam, int32_t world_size, int32_t tile_w, int32_t tile_h, int64_t capacity,
+                 const void* d_in, void* d_frame, uint32_t E, void* stream) {
+    if (!cam || !d_in || !d_frame || capacity < 0 || world_size < 1 || tile_w < 1 || tile_h < 1 ||
+        cam->image_width < 1 || cam->image_height < 1)
+        return fail(GS_ERR_ARG, "bad argument");
+    if (capacity % ((int64_t)tile_w * tile_h) != 0) return fail(GS_ERR_ARG, "capacity is not whole tiles");
+    if (capacity == 0) return GS_OK;
+    const int32_t W = cam->image_width, H = cam->image_height;
+    const int32_t tiles_x = (W + tile_w - 1) / tile_w;
+    auto fits = [&](uint64_t v) {
+        return ((uint64_t)W * E) % v == 0 && ((uint64_t)tile_w * E) % v == 0 && ((uintptr_t)d_in % v) == 0 &&
+               ((uintptr_t)d_frame % v) == 0;
+    };
+    const int vec = fits(16) ? 16 : (fits(4) ? 4 : 1);
+    const uint64_t units = (uint64_t)capacity * E * (uint64_t)world_size / (uint64_t)vec;
+    const unsigned grid = (unsigned)std::min<uint64_t>((units + 255) / 256, 8192);
+    hipStream_t st = (hipStream_t)stream;
+    const uint8_t* in = (const uint8_t*)d_in;
+    uint8_t* fr = (uint8_t*)d_frame;
+    if (vec == 16)
+        hipLaunchKernelGGL(gs_unpack_kernel<16>, dim3(grid), dim3(256), 0, st, in, fr, E, W, H, world_size, tile_w,
+                           tile_h, tiles_x, (uint64_t)capacity);
+    else if (vec == 4)
+        hipLaunchKernelGGL(gs_unpack_kernel<4>, dim3(grid), dim3(256), 0, st, in, fr, E, W, H, world_size, tile_w,
+                           tile_h, tiles_x, (uint64_t)capacity);
+    else
+        hipLaunchKernelGGL(gs_unpack_kernel<1>, dim3(grid), dim3(256), 0, st, in, fr, E, W, H, world_size, tile_w,
+                           tile_h, tiles_x, (uint64_t)capacity);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(GS_ERR_HIP, hipGetErrorString(e));
+    return GS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -220,7 +288,7 @@ int64_t gs_ppm_max_bytes(int32_t width, int32_t height) {
 
 int64_t gs_ppm_scratch_bytes(int32_t width, int32_t height) {
     if (width <= 0 || height <= 0) return -1;
-    return 64 + (int64_t)ppm_blocks(width, height) * 8;  // ticket (padded to 64 B) + one status word per block
+    return (int64_t)ppm_blocks(width, height) * 8;  // one length / offset per block
 }
 
 gs_status gs_ppm_encode_async(const uint8_t* d_rgb8, int32_t width, int32_t height, char* d_text,
@@ -231,38 +299,30 @@ gs_status gs_ppm_encode_async(const uint8_t* d_rgb8, int32_t width, int32_t heig
     if ((uint64_t)width * (uint64_t)height >= (1ull << 40)) return fail(GS_ERR_ARG, "image too large");
     if (text_capacity < gs_ppm_max_bytes(width, height)) return fail(GS_ERR_ARG, "text capacity below gs_ppm_max_bytes");
     if (scratch_bytes < gs_ppm_scratch_bytes(width, height)) return fail(GS_ERR_ARG, "scratch below gs_ppm_scratch_bytes");
-    if (((uintptr_t)d_rgb8 & 3u) || ((uintptr_t)d_text & 3u) || ((uintptr_t)d_scratch & 7u))
-        return fail(GS_ERR_ARG, "rgb8 and text must be 4-byte aligned, scratch 8-byte aligned");
+    if (((uintptr_t)d_rgb8 & 3u) || ((uintptr_t)d_text & 15u) || ((uintptr_t)d_scratch & 7u))
+        return fail(GS_ERR_ARG, "rgb8 must be 4-byte aligned, text 16-byte aligned, scratch 8-byte aligned");
     PpmHeader h;
     header_of(width, height, &h);
     const uint32_t nb = ppm_blocks(width, height);
+    const uint64_t n_px = (uint64_t)width * (uint64_t)height;
     hipStream_t st = (hipStream_t)stream;
-    hipError_t e = hipMemsetAsync(d_scratch, 0, (size_t)gs_ppm_scratch_bytes(width, height), st);
-    if (e != hipSuccess) return fail(GS_ERR_HIP, hipGetErrorString(e));
-    uint32_t* ticket = (uint32_t*)d_scratch;
-    unsigned long long* status = (unsigned long long*)((char*)d_scratch + 64);
-    hipLaunchKernelGGL(gs_ppm_kernel, dim3(nb), dim3(PPM_THREADS), 0, st, d_rgb8,
-                       (uint64_t)width * (uint64_t)height, d_text, d_len, status, ticket, nb, h);
-    e = hipGetLastError();
+    uint64_t* blk = (uint64_t*)d_scratch;
+    hipLaunchKernelGGL(gs_ppm_size_kernel, dim3(nb), dim3(PPM_THREADS), 0, st, d_rgb8, n_px, blk);
+    hipLaunchKernelGGL(gs_ppm_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, st, blk, nb, d_text, d_len, h);
+    hipLaunchKernelGGL(gs_ppm_kernel, dim3(nb), dim3(PPM_THREADS), 0, st, d_rgb8, n_px, (const uint64_t*)blk, d_text);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(GS_ERR_HIP, hipGetErrorString(e));
     return GS_OK;
 }
 
 gs_status gs_unpack_tiles_u8_async(const gs_camera* cam, int32_t world_size, int32_t tile_w, int32_t tile_h,
                                    int64_t capacity, const uint8_t* d_in, uint8_t* d_frame, void* stream) {
-    if (!cam || !d_in || !d_frame || capacity < 0 || world_size < 1 || tile_w < 1 || tile_h < 1 ||
-        cam->image_width < 1 || cam->image_height < 1)
-        return fail(GS_ERR_ARG, "bad argument");
-    if (capacity % ((int64_t)tile_w * tile_h) != 0) return fail(GS_ERR_ARG, "capacity is not whole tiles");
-    if (capacity == 0) return GS_OK;
-    const int32_t tiles_x = (cam->image_width + tile_w - 1) / tile_w;
-    const uint64_t total = (uint64_t)capacity * world_size;
-    const unsigned grid = (unsigned)std::min<uint64_t>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(gs_unpack_u8_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_in, d_frame,
-                       cam->image_width, cam->image_height, world_size, tile_w, tile_h, tiles_x, (uint64_t)capacity);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(GS_ERR_HIP, hipGetErrorString(e));
-    return GS_OK;
+    return unpack(cam, world_size, tile_w, tile_h, capacity, d_in, d_frame, 3, stream);
+}
+
+gs_status gs_unpack_tiles_async(const gs_camera* cam, int32_t world_size, int32_t tile_w, int32_t tile_h,
+                                int64_t capacity, const float* d_in, float* d_frame, void* stream) {
+    return unpack(cam, world_size, tile_w, tile_h, capacity, d_in, d_frame, 12, stream);
 }
 
 }  // extern "C"

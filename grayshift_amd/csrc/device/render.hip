@@ -1008,27 +1008,6 @@ __global__ void gs_combine_kernel(const KParams* __restrict__ P) {
     }
 }
 
-// Scatter rank-packed tiles into the frame.
-__global__ void gs_unpack_kernel(const float* __restrict__ in, float* __restrict__ frame, int32_t W, int32_t H,
-                                 int32_t world, int32_t tile_w, int32_t tile_h, int32_t tiles_x, uint64_t capacity) {
-    const uint64_t total = capacity * (uint64_t)world;
-    const uint32_t tile_px = (uint32_t)(tile_w * tile_h);
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total; g += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t r = (uint32_t)(g / capacity);
-        const uint64_t k = g % capacity;
-        const uint32_t slot = (uint32_t)(k / tile_px), w = (uint32_t)(k % tile_px);
-        const uint32_t tile = r + slot * (uint32_t)world;
-        const int32_t x = (int32_t)((tile % (uint32_t)tiles_x) * (uint32_t)tile_w + w % (uint32_t)tile_w);
-        const int32_t y = (int32_t)((tile / (uint32_t)tiles_x) * (uint32_t)tile_h + w / (uint32_t)tile_w);
-        if (x < W && y < H) {
-            const size_t o = ((size_t)y * (size_t)W + (size_t)x) * 3;
-            frame[o] = in[g * 3];
-            frame[o + 1] = in[g * 3 + 1];
-            frame[o + 2] = in[g * 3 + 2];
-        }
-    }
-}
-
 // =============================================================== host side
 static thread_local std::string tl_err;
 static int32_t g_shade_batch = 52;  // swept on MI355X C4 (chunked, uniform loop): 48 -> 3502, 52 -> 3535-3568, 56 -> 3506-3536 Msamples/s
@@ -1526,21 +1505,6 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
         hipLaunchKernelGGL(gs_combine_kernel, dim3(grid), dim3(256), 0, st, (const KParams*)ds->params);
         HIPCHK(hipGetLastError());
     }
-    return GS_OK;
-}
-
-gs_status gs_unpack_tiles_async(const gs_camera* cam, int32_t world_size, int32_t tile_w, int32_t tile_h,
-                                int64_t capacity, const float* d_in, float* d_frame, void* stream) {
-    gs_partition p{0, world_size, tile_w, tile_h};
-    if (!part_ok(cam, &p) || !d_in || !d_frame || capacity < 0) return fail(GS_ERR_ARG, "bad argument");
-    if (capacity % ((int64_t)tile_w * tile_h) != 0) return fail(GS_ERR_ARG, "capacity is not whole tiles");
-    if (capacity == 0) return GS_OK;
-    int32_t tiles_x = (cam->image_width + tile_w - 1) / tile_w;
-    uint64_t total = (uint64_t)capacity * world_size;
-    unsigned grid = (unsigned)std::min<uint64_t>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(gs_unpack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_in, d_frame,
-                       cam->image_width, cam->image_height, world_size, tile_w, tile_h, tiles_x, (uint64_t)capacity);
-    HIPCHK(hipGetLastError());
     return GS_OK;
 }
 

@@ -263,14 +263,15 @@ gs_status gs_unpack_tiles_u8_async(const gs_camera* cam, int32_t world_size, int
 /* ---- Output stage on the device (camera.rs:101-103,116-118; color.rs:8-18) (ABI 3) ----
  * The reference writes an ASCII PPM: "P3\n{W} {H}\n255\n", then one "{r} {g} {b}\n"
  * line per pixel in row-major order.  gs_ppm_encode_async formats that text on the
- * device from a W*H*3 byte frame (rgb8 output, unpacked), in one pass: each block
- * formats 2048 pixels in LDS and finds its output offset by a decoupled look-back over
- * its predecessors' lengths.  The host writes the result with one write call. */
+ * device from a W*H*3 byte frame (rgb8 output, unpacked): per-block text lengths, one
+ * scan into offsets, then each block formats 2048 pixels in LDS and streams them out.
+ * The host writes the result with one write call. */
 int64_t gs_ppm_max_bytes(int32_t width, int32_t height);     /* text capacity bound */
 int64_t gs_ppm_scratch_bytes(int32_t width, int32_t height); /* device scratch size */
-/* d_rgb8: device, W*H*3 bytes; d_text: device, >= gs_ppm_max_bytes; d_len: device
- * int64, receives the text length; d_scratch: device, >= gs_ppm_scratch_bytes (its
- * contents are overwritten; it may be reused after the stream has passed this call). */
+/* d_rgb8: device, W*H*3 bytes, 4-byte aligned; d_text: device, >= gs_ppm_max_bytes,
+ * 16-byte aligned (hipMalloc'd buffers are); d_len: device
+ * int64, receives the text length; d_scratch: device, >= gs_ppm_scratch_bytes, 8-byte
+ * aligned (overwritten; reusable once the stream has passed this call). */
 gs_status gs_ppm_encode_async(const uint8_t* d_rgb8, int32_t width, int32_t height, char* d_text,
                               int64_t text_capacity, int64_t* d_len, void* d_scratch,
                               int64_t scratch_bytes, void* stream);

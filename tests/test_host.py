@@ -259,8 +259,8 @@ def test_ppm_sizes():
     hdr = len(b"P3\n3840 2160\n255\n")
     assert N.lib.gs_ppm_max_bytes(3840, 2160) == hdr + 3840 * 2160 * 12
     assert N.lib.gs_ppm_max_bytes(0, 5) == -1 and N.lib.gs_ppm_scratch_bytes(5, -1) == -1
-    assert N.lib.gs_ppm_scratch_bytes(1, 1) == 64 + 8
-    assert N.lib.gs_ppm_scratch_bytes(2048, 1) == 64 + 8 and N.lib.gs_ppm_scratch_bytes(2049, 1) == 64 + 16
+    assert N.lib.gs_ppm_scratch_bytes(1, 1) == 8
+    assert N.lib.gs_ppm_scratch_bytes(2048, 1) == 8 and N.lib.gs_ppm_scratch_bytes(2049, 1) == 16
 
 
 def test_ppm_encode_rejects_bad_arguments_before_the_device():
@@ -270,6 +270,6 @@ def test_ppm_encode_rejects_bad_arguments_before_the_device():
     assert N.lib.gs_ppm_encode_async(ok, 0, 4, ok, 1 << 20, ok, ok, 1 << 20, None) == N.GS_ERR_ARG
     assert N.lib.gs_ppm_encode_async(ok, 4, 4, ok, 10, ok, ok, 1 << 20, None) == N.GS_ERR_ARG
     assert b"capacity" in N.lib.gs_last_error()
-    assert N.lib.gs_ppm_encode_async(ok, 4, 4, ok, 1 << 20, ok, ok, 8, None) == N.GS_ERR_ARG
+    assert N.lib.gs_ppm_encode_async(ok, 4, 4, ok, 1 << 20, ok, ok, 4, None) == N.GS_ERR_ARG
     assert N.lib.gs_ppm_encode_async(P(0x1001), 4, 4, ok, 1 << 20, ok, ok, 1 << 20, None) == N.GS_ERR_ARG
     assert b"aligned" in N.lib.gs_last_error()
