@@ -24,6 +24,8 @@ pub const GS_REF_QUAD: u32 = 4;
 pub const GS_REF_TRIANGLE: u32 = 5;
 pub const GS_REF_LIST: u32 = 6;
 pub const GS_REF_INSTANCE: u32 = 7;
+pub const GS_REF_MEDIUM: u32 = 8;
+pub const GS_ABI_VERSION: i32 = 3;
 pub const fn gs_make_ref(kind: u32, idx: u32) -> u32 { (kind << GS_REF_SHIFT) | (idx & 0x0FFF_FFFF) }
 
 #[repr(C)] #[derive(Clone, Copy, Default)]
@@ -42,6 +44,9 @@ pub const GS_INST_TRANSLATE: u32 = 1;
 pub const GS_INST_ROTATE_Y: u32 = 2;
 #[repr(C)] #[derive(Clone, Copy, Default)]
 pub struct gs_instance { pub kind: u32, pub child: u32, pub p: [f64; 3] }
+/// ConstantMedium (hittable/volume.rs:10-29) (ABI 2).
+#[repr(C)] #[derive(Clone, Copy, Default)]
+pub struct gs_medium { pub boundary: u32, pub material: u32, pub density_neg_inv: f64 }
 #[repr(C)] #[derive(Clone, Copy, Default)]
 pub struct gs_material { pub kind: u32, pub texture: u32, pub albedo: [f64; 3], pub param: f64 }
 #[repr(C)] #[derive(Clone, Copy, Default)]
@@ -68,6 +73,7 @@ pub struct gs_flat_scene {
     pub texels8: *const u8, pub n_texels8: u64,
     pub background: gs_background,
     pub hdri_rgb: *const f32, pub n_hdri_floats: u64,
+    pub media: *const gs_medium, pub n_media: u32,
 }
 
 /// The fields `Camera::new` derives (camera.rs:17-98).
@@ -91,8 +97,13 @@ pub struct gs_counters {
     pub rays: u64, pub node_visits: u64, pub sphere_tests: u64, pub msphere_tests: u64,
     pub quad_tests: u64, pub tri_tests: u64, pub instance_tests: u64, pub list_tests: u64,
     pub hits: u64, pub image_texels: u64, pub hdri_texels: u64, pub paths: u64, pub pixels: u64,
-    pub reserved: [u64; 3],
+    pub medium_tests: u64, pub reserved: [u64; 2],
 }
+
+/// Outputs of one launch (ABI 3): either or both of the linear f32 colour and
+/// write_color's bytes of the f64 colour, per packed pixel.
+#[repr(C)]
+pub struct gs_render_outputs { pub rgb: *mut f32, pub rgb8: *mut u8, pub item_visits: *mut u32 }
 
 #[repr(C)] pub struct gs_device_scene { _private: [u8; 0] }
 
@@ -113,6 +124,21 @@ extern "C" {
                                        d_item_visits: *mut u32, stream: *mut c_void) -> gs_status;
     pub fn gs_unpack_tiles_async(cam: *const gs_camera, world_size: i32, tile_w: i32, tile_h: i32, capacity: i64,
                                  d_gathered: *const f32, d_frame: *mut f32, stream: *mut c_void) -> gs_status;
+    pub fn gs_render_tiles_ex_async(scene: *const gs_device_scene, cam: *const gs_camera,
+                                    ss: *const gs_sample_settings, seed: u64, part: *const gs_partition,
+                                    out: *const gs_render_outputs, d_counters: *mut gs_counters,
+                                    stream: *mut c_void) -> gs_status;
+    pub fn gs_unpack_tiles_u8_async(cam: *const gs_camera, world_size: i32, tile_w: i32, tile_h: i32, capacity: i64,
+                                    d_gathered: *const u8, d_frame: *mut u8, stream: *mut c_void) -> gs_status;
+    pub fn gs_ppm_max_bytes(width: i32, height: i32) -> i64;
+    pub fn gs_ppm_scratch_bytes(width: i32, height: i32) -> i64;
+    pub fn gs_ppm_encode_async(d_rgb8: *const u8, width: i32, height: i32, d_text: *mut c_char, text_capacity: i64,
+                               d_len: *mut i64, d_scratch: *mut c_void, scratch_bytes: i64,
+                               stream: *mut c_void) -> gs_status;
+    /// The whole of camera.rs:100-121 past the world build: PPM text into `out_text`.
+    pub fn gs_render_ppm(scene: *const gs_flat_scene, cam: *const gs_camera, ss: *const gs_sample_settings, seed: u64,
+                         out_text: *mut c_char, text_capacity: i64, out_len: *mut i64,
+                         counters: *mut gs_counters) -> gs_status;
     /// The one-call replacement of camera.rs:105-114.
     pub fn gs_render(scene: *const gs_flat_scene, cam: *const gs_camera, ss: *const gs_sample_settings, seed: u64,
                      out_rgb: *mut f32, counters: *mut gs_counters) -> gs_status;
@@ -120,4 +146,20 @@ extern "C" {
 
 pub fn last_error() -> String {
     unsafe { std::ffi::CStr::from_ptr(gs_last_error()).to_string_lossy().into_owned() }
+}
+
+/// `Camera::render` (camera.rs:100-121) on the device: flatten, render, write the
+/// device-formatted PPM text with one call.  `flat`, `cam` and `ss` come from the
+/// crate's `flatten` trait method and `Camera::new`.
+pub fn render_ppm(flat: &gs_flat_scene, cam: &gs_camera, ss: &gs_sample_settings, seed: u64,
+                  out: &mut impl std::io::Write) -> std::io::Result<()> {
+    let cap = unsafe { gs_ppm_max_bytes(cam.image_width, cam.image_height) };
+    if cap < 0 { return Err(std::io::Error::new(std::io::ErrorKind::InvalidInput, "bad image size")); }
+    let mut text = vec![0u8; cap as usize];
+    let mut len: i64 = 0;
+    let st = unsafe {
+        gs_render_ppm(flat, cam, ss, seed, text.as_mut_ptr() as *mut c_char, cap, &mut len, std::ptr::null_mut())
+    };
+    if st != GS_OK { return Err(std::io::Error::new(std::io::ErrorKind::Other, last_error())); }
+    out.write_all(&text[..len as usize])
 }

@@ -273,3 +273,37 @@ def test_ppm_encode_rejects_bad_arguments_before_the_device():
     assert N.lib.gs_ppm_encode_async(ok, 4, 4, ok, 1 << 20, ok, ok, 4, None) == N.GS_ERR_ARG
     assert N.lib.gs_ppm_encode_async(P(0x1001), 4, 4, ok, 1 << 20, ok, ok, 1 << 20, None) == N.GS_ERR_ARG
     assert b"aligned" in N.lib.gs_last_error()
+
+
+# ------------------------------------------------- Rust binding
+def _rust():
+    return open(os.path.join(ROOT, "bindings", "grayshift_gpu.rs")).read()
+
+
+def test_rust_binding_declares_every_gpu_entry_point():
+    src = open(os.path.join(ROOT, "include", "grayshift_gpu.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    c_fns = set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s*(gs_[a-z0-9_]+)\s*\(", src, re.M))
+    rs_fns = set(re.findall(r"pub fn (gs_[a-z0-9_]+)\s*\(", _rust()))
+    assert c_fns == rs_fns
+    assert "pub const GS_ABI_VERSION: i32 = %d;" % N.GS_ABI_VERSION in _rust()
+
+
+@pytest.mark.parametrize("name", ["gs_counters", "gs_flat_scene", "gs_camera", "gs_render_outputs", "gs_medium"])
+def test_rust_struct_fields_follow_the_header(name):
+    """Field names in declaration order (arrays flattened by name) match the C struct."""
+    hdrs = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("grayshift_gpu.h", "grayshift_scene.h"))
+    hdrs = re.sub(r"/\*.*?\*/", "", hdrs, flags=re.S)
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), hdrs, re.S).group(1)
+    c_names = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        for part in decl.split(","):
+            m = re.search(r"([A-Za-z_][A-Za-z0-9_]*)\s*(\[[^\]]*\])?\s*$", part.strip())
+            c_names.append(m.group(1))
+    rs = re.search(r"pub struct %s \{(.*?)\}" % name, _rust(), re.S).group(1)
+    rs_names = re.findall(r"pub ([a-z_0-9]+)\s*:", rs)
+    norm = {"min": "mn", "max": "mx"}
+    assert [norm.get(n, n) for n in rs_names] == [norm.get(n, n) for n in c_names]
