@@ -26,7 +26,8 @@ sys.path.insert(0, ROOT)
 # Algorithmic bytes per unit: what the reference
 # algorithm reads for each counted event.
 BYTES = {"node_visits": 56, "sphere_tests": 40, "msphere_tests": 64, "quad_tests": 136, "tri_tests": 104,
-         "instance_tests": 32, "medium_tests": 16, "hits": 32, "image_texels": 3, "hdri_texels": 12, "pixels": 12}
+         "instance_tests": 32, "medium_tests": 16, "hits": 32, "image_texels": 3, "hdri_texels": 12, "pixels": 12,
+         "noise_evals": 168}  # noise: 7 octaves x 8 corners x 3 permutation-table bytes
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 

@@ -74,6 +74,7 @@ pub struct gs_flat_scene {
     pub background: gs_background,
     pub hdri_rgb: *const f32, pub n_hdri_floats: u64,
     pub media: *const gs_medium, pub n_media: u32,
+    pub noise_perm: *const u8, pub n_noise_perm: u32,
 }
 
 /// The fields `Camera::new` derives (camera.rs:17-98).
@@ -97,7 +98,7 @@ pub struct gs_counters {
     pub rays: u64, pub node_visits: u64, pub sphere_tests: u64, pub msphere_tests: u64,
     pub quad_tests: u64, pub tri_tests: u64, pub instance_tests: u64, pub list_tests: u64,
     pub hits: u64, pub image_texels: u64, pub hdri_texels: u64, pub paths: u64, pub pixels: u64,
-    pub medium_tests: u64, pub reserved: [u64; 2],
+    pub medium_tests: u64, pub noise_evals: u64, pub reserved: [u64; 1],
 }
 
 /// Outputs of one launch (ABI 3): either or both of the linear f32 colour and

@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("GS_LIB") or os.path.join(HERE, "libgrayshift.so")  # 
 GS_OBJ_SPHERE, GS_OBJ_MOVING_SPHERE, GS_OBJ_QUAD, GS_OBJ_TRIANGLE = 1, 2, 3, 4
 GS_OBJ_LIST, GS_OBJ_BVH, GS_OBJ_TRANSLATE, GS_OBJ_ROTATE_Y, GS_OBJ_CUBE, GS_OBJ_MEDIUM = 5, 6, 7, 8, 9, 10
 GS_MAT_LAMBERTIAN, GS_MAT_METAL, GS_MAT_DIELECTRIC, GS_MAT_DIFFUSE_LIGHT, GS_MAT_ISOTROPIC = 1, 2, 3, 4, 5
-GS_TEX_SOLID, GS_TEX_CHECKERED, GS_TEX_IMAGE = 1, 2, 3
+GS_TEX_SOLID, GS_TEX_CHECKERED, GS_TEX_IMAGE, GS_TEX_NOISE = 1, 2, 3, 4
 GS_BG_SOLID, GS_BG_HDRI = 1, 2
 GS_ABI_VERSION = 3
 GS_OK, GS_ERR_ARG, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPORTED, GS_ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5
@@ -68,11 +68,11 @@ class gs_sample_settings(C.Structure):
 
 COUNTER_NAMES = ["rays", "node_visits", "sphere_tests", "msphere_tests", "quad_tests", "tri_tests",
                  "instance_tests", "list_tests", "hits", "image_texels", "hdri_texels", "paths", "pixels",
-                 "medium_tests"]
+                 "medium_tests", "noise_evals"]
 
 
 class gs_counters(C.Structure):
-    _fields_ = [(n, C.c_uint64) for n in COUNTER_NAMES] + [("reserved", C.c_uint64 * 2)]
+    _fields_ = [(n, C.c_uint64) for n in COUNTER_NAMES] + [("reserved", C.c_uint64 * 1)]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n in COUNTER_NAMES}
@@ -114,7 +114,8 @@ class gs_flat_scene(C.Structure):
                 ("texels8", C.c_void_p), ("n_texels8", C.c_uint64),
                 ("background", gs_background),
                 ("hdri_rgb", C.c_void_p), ("n_hdri_floats", C.c_uint64),
-                ("media", C.c_void_p), ("n_media", C.c_uint32)]
+                ("media", C.c_void_p), ("n_media", C.c_uint32),
+                ("noise_perm", C.c_void_p), ("n_noise_perm", C.c_uint32)]
 
 
 class gs_render_outputs(C.Structure):
@@ -160,6 +161,7 @@ SIGNATURES = {
                                             C.POINTER(C.c_int64), C.POINTER(gs_counters)]),
     "gs_host_write_ppm": (C.c_int32, [C.c_char_p, C.c_int32, C.c_int32, _P]),
     "gs_host_color_byte": (C.c_int32, [C.c_double]),
+    "gs_host_noise_permutation": (None, [C.c_uint32, _P]),
     "gs_host_bvh_topology": (C.c_int64, [C.POINTER(gs_scene_spec), C.POINTER(C.c_int32), C.c_int64]),
     "gs_host_struct_size": (C.c_int64, [C.c_char_p]),
 }

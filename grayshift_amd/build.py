@@ -31,6 +31,7 @@ SOURCES = [
 DEPS = SOURCES + [
     os.path.join(HERE, "csrc", "device", "devmath.hpp"),
     os.path.join(HERE, "csrc", "device", "geometry.hpp"),
+    os.path.join(HERE, "csrc", "device", "perlin.hpp"),
     os.path.join(HERE, "csrc", "host", "world.hpp"),
     os.path.join(ROOT, "include", "grayshift_gpu.h"),
     os.path.join(ROOT, "include", "grayshift_host.h"),

@@ -102,6 +102,16 @@ __device__ __forceinline__ bool box_hit(const DNode& n, const d3& o, const d3& i
     return !(hi <= lo);
 }
 
+// box_hit with a per-lane tmin (no SGPR operand): for walks whose interval is not
+// wave-uniform by construction (the nested BVH walk).
+__device__ __forceinline__ bool box_hit_v(const DNode& n, const d3& o, const d3& inv, double tmin, double tmax) {
+    double lo = tmin, hi = tmax;
+    slab(n.mnx, n.mxx, o.x, inv.x, lo, hi);
+    slab(n.mny, n.mxy, o.y, inv.y, lo, hi);
+    slab(n.mnz, n.mxz, o.z, inv.z, lo, hi);
+    return !(hi <= lo);
+}
+
 // Rays whose slab times can never be NaN — every 1/d finite and non-zero, |origin| and
 // every box coordinate below 1e300 (so mn - o is finite; finite x finite non-zero is
 // never NaN) — take the swap as (min, max): for non-NaN t0 != t1 that is exactly the

@@ -34,6 +34,7 @@
 #include "../../../include/grayshift_gpu.h"
 #include "devmath.hpp"
 #include "geometry.hpp"
+#include "perlin.hpp"
 
 using namespace gsd;
 
@@ -48,6 +49,10 @@ using namespace gsd;
 #define GS_MIN_WAVES 4
 #endif
 #define GS_MAX_CHAIN 4
+#define GS_NESTED_STACK 32  // max depth of a BVH under a Translate/RotateY chain
+// Kernel feature flags (template argument): scenes without them compile the code out.
+#define GS_FEAT_MEDIA 1   // ConstantMedium leaves (RNG draws inside traversal)
+#define GS_FEAT_NESTED 2  // BVHs under Translate/RotateY (a second-level walk, private stack)
 
 // ---------------------------------------------------------------- device layout
 // Internal layouts (may differ from the ABI records; converted at upload).
@@ -73,7 +78,7 @@ struct alignas(16) DMaterial {
     double pad2;
 };
 
-enum { C_RAYS = 0, C_NODES, C_SPH, C_MSPH, C_QUAD, C_TRI, C_INST, C_LIST, C_HITS, C_IMG, C_HDRI, C_PATHS, C_PIX, C_MED, C_N };
+enum { C_RAYS = 0, C_NODES, C_SPH, C_MSPH, C_QUAD, C_TRI, C_INST, C_LIST, C_HITS, C_IMG, C_HDRI, C_PATHS, C_PIX, C_MED, C_NOISE, C_N };
 
 struct DevScene {
     const DNode* nodes;
@@ -86,6 +91,7 @@ struct DevScene {
     const uint32_t* list_refs;
     const gs_instance* inst;
     const gs_medium* media;
+    const uint8_t* noise_perm;  // 256 B, Perlin::default()'s table (NoiseTexture)
     const DMaterial* mats;
     const gs_texture* texs;
     const gs_image* images;
@@ -250,12 +256,48 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, uint32_t cur, co
     res.inst = inst_ref;
 }
 
+// A BVH under a Translate/RotateY chain (final_scene's rotated box of balls, main.rs:
+// 741-755): BVHNode::hit (BVH.rs:69-90) on the ray in the instance's space, as the same
+// left-first walk with a shrinking closest t as the top level, on a private stack.
+// `root`: a device node ref.  Leaves are lists or primitives (validated on the host).
+__device__ __forceinline__ void nested_bvh(const DevScene& sc, uint32_t root, const Ray& r, double tmin,
+                                           double closest, uint32_t inst_ref, LeafHit& res,
+                                           unsigned long long* cnt) {
+    // AABB::hit's `1.0 / ray.direction[axis]` (AABB.rs:64), hoisted per ray (same value)
+    const d3 inv = mk(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
+    uint32_t stk[GS_NESTED_STACK];
+    uint32_t sp = 0, cur = root;
+#pragma unroll 1
+    for (;;) {
+        if (cur == DREF_NONE) {
+            if (sp == 0) break;
+            cur = stk[--sp];
+            continue;
+        }
+        if (cur < DREF_LEAF) {
+            atomicAdd(&cnt[C_NODES], 1ull);
+            const DNode n = load_node(sc.nodes + cur);
+            if (box_hit_v(n, r.o, inv, tmin, closest)) {
+                if (n.right != DREF_NONE) stk[sp++] = n.right;
+                cur = n.left;
+            } else {
+                cur = DREF_NONE;
+            }
+        } else {
+            shape_test(sc, cur, r, tmin, closest, inst_ref, res, cnt);
+            if (res.hit) closest = res.t;  // res.t only ever shrinks
+            cur = DREF_NONE;
+        }
+    }
+}
+
 // The rarer non-node children (everything but a stationary sphere reached directly
-// from a BVH node): moving sphere, quad, triangle, HittableList, ConstantMedium, behind
-// an optional Translate/RotateY chain.  `rng`: a medium draws from the lane's stream.
-// MEDIA is a kernel template flag: scenes without media compile the medium test out
-// (it costs the traversal loop 4 VGPRs and spills otherwise).
-template <bool MEDIA>
+// from a BVH node): moving sphere, quad, triangle, HittableList, ConstantMedium, a BVH
+// under an instance, behind an optional Translate/RotateY chain.  `rng`: a medium draws
+// from the lane's stream.  FEAT (GS_FEAT_*) is a kernel template argument: scenes
+// without media / nested BVHs compile those out (the medium test costs the traversal
+// loop 4 VGPRs and spills otherwise; the nested walk uses private memory).
+template <int FEAT>
 __device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, uint32_t ref, Ray r, double tmin, double closest,
                                            uint64_t& rng, unsigned long long* cnt) {
     LeafHit res;
@@ -265,8 +307,10 @@ __device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, uint32_t ref, Ray 
     res.inst = GS_REF_NONE;
     const uint32_t inst_ref = (ref >> GS_REF_SHIFT) == GS_REF_INSTANCE ? ref : GS_REF_NONE;
     const uint32_t cur = walk_chain(sc, ref, r, cnt);
-    if (MEDIA && (cur >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
+    if ((FEAT & GS_FEAT_MEDIA) && (cur >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
         medium_test(sc, cur, r, tmin, closest, inst_ref, rng, res, cnt);
+    } else if ((FEAT & GS_FEAT_NESTED) && (cur >> GS_REF_SHIFT) == GS_REF_NODE) {
+        nested_bvh(sc, cur & GS_REF_MASK, r, tmin, closest, inst_ref, res, cnt);
     } else {
         shape_test(sc, cur, r, tmin, closest, inst_ref, res, cnt);
     }
@@ -377,6 +421,11 @@ __device__ GS_NOINLINE d3 texture_value(const DevScene& sc, uint32_t tex, double
             int32_t s = (int32_t)((uint32_t)xi + (uint32_t)yi + (uint32_t)zi);
             tex = (s % 2 == 0) ? t.even : t.odd;
             continue;
+        }
+        if (t.kind == GS_TEX_NOISE) {  // texture.rs:127-130
+            atomicAdd(&cnt[C_NOISE], 1ull);
+            const double n = noise_value(sc.noise_perm, t.color[0], p.x, p.y, p.z);
+            return mk(n, n, n);
         }
         // GS_TEX_IMAGE
         const gs_image im = sc.images[t.image];
@@ -547,7 +596,7 @@ __host__ __device__ inline size_t lds_bytes(uint32_t stack_depth) {
     return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4 + (stack_depth + 1) * 4);  // + the dummy slot 0
 }
 
-template <bool MEDIA>
+template <int FEAT>
 __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs A) {
     extern __shared__ __align__(16) uint8_t smem[];
     __shared__ unsigned long long s_cnt[C_N];
@@ -849,7 +898,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         hit_inst = GS_REF_NONE;
                     }
                 } else {
-                    const LeafHit lh = leaf_other<MEDIA>(sc, cur, ray, tmin, closest, rng, s_cnt);
+                    const LeafHit lh = leaf_other<FEAT>(sc, cur, ray, tmin, closest, rng, s_cnt);
                     if (lh.hit) {
                         closest = lh.t;
                         hit_ref = lh.ref;
@@ -1036,7 +1085,7 @@ struct gs_device_scene {
     uint32_t n_nodes = 0;
     uint32_t stack_depth = 1;  // LDS stack entries per lane (= BVH depth)
     bool fast_boxes = false;  // every node coordinate |x| < 1e300
-    bool has_media = false;   // launch gs_render_kernel<true>
+    int feat = 0;             // GS_FEAT_* of the kernel instantiation to launch
     double* partial = nullptr;  // chunk partial sums, grown on demand
     size_t partial_bytes = 0;
 };
@@ -1055,7 +1104,7 @@ struct Layout {
 
 // Host-side validation of everything the kernel indexes, so a malformed scene is an
 // error code, never a GPU fault.
-gs_status validate(const gs_flat_scene& s, uint32_t* depth_out) {
+gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out) {
     auto bad = [](const std::string& m) { return fail(GS_ERR_ARG, "invalid flat scene: " + m); };
     auto unsup = [](const std::string& m) { return fail(GS_ERR_UNSUPPORTED, m); };
     if (!s.nodes && s.n_nodes) return bad("nodes");
@@ -1101,10 +1150,37 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out) {
         if (k == GS_REF_NODE || k == GS_REF_MEDIUM || k == GS_REF_INSTANCE) return 2;
         return prim_ok(cur) ? 0 : 1;
     };
+    // A BVH under an instance chain: nodes in range, leaves lists or primitives, depth
+    // within the device's private stack.  Subtrees may be shared between chains
+    // (instancing); the depth bound ends cycles and a visit budget ends blow-ups.
+    bool nested = false;
+    uint64_t nested_budget = 64ull << 20;
+    auto nested_ok = [&](uint32_t root) -> int {
+        std::vector<std::pair<uint32_t, uint32_t>> st{{root, 1u}};
+        while (!st.empty()) {
+            auto [r, d] = st.back();
+            st.pop_back();
+            if (nested_budget-- == 0) return 1;
+            if ((r >> GS_REF_SHIFT) == GS_REF_NODE) {
+                const uint32_t i = r & GS_REF_MASK;
+                if (i >= s.n_nodes) return 1;
+                if (d > GS_NESTED_STACK) return 2;
+                if (s.nodes[i].left == GS_REF_NONE) return 1;
+                st.push_back({s.nodes[i].left, d + 1});
+                if (s.nodes[i].right != GS_REF_NONE) st.push_back({s.nodes[i].right, d + 1});
+            } else {
+                const int e = shape_ok(r);
+                if (e) return e;
+            }
+        }
+        nested = true;
+        return 0;
+    };
     auto leaf_ok = [&](uint32_t r) -> int {  // 0 ok, 1 bad, 2 unsupported
         uint32_t cur = r;
         int e = chain_ok(cur);
         if (e) return e;
+        if ((cur >> GS_REF_SHIFT) == GS_REF_NODE && cur != r) return nested_ok(cur);
         if ((cur >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
             uint32_t i = cur & GS_REF_MASK;
             if (i >= s.n_media || !s.media) return 1;
@@ -1137,12 +1213,15 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out) {
         } else {
             int e = leaf_ok(r);
             if (e == 1) return bad("leaf reference");
-            if (e == 2) return unsup("instance chain deeper than 4, BVH under an instance or inside a medium "
-                                     "boundary, nested media, or a list member that is not a primitive");
+            if (e == 2) return unsup("instance chain deeper than 4, a BVH under an instance deeper than " +
+                                     std::to_string(GS_NESTED_STACK) + " or with leaves that are not lists or "
+                                     "primitives, a BVH inside a medium boundary, nested media, or a list member "
+                                     "that is not a primitive");
         }
     }
     if (maxd > GS_STACK) return unsup("BVH deeper than the device stack (" + std::to_string(GS_STACK) + ")");
     *depth_out = maxd;
+    *nested_out = nested;
     auto mat_ok = [&](uint32_t m) { return m < s.n_materials; };
     for (uint32_t i = 0; i < s.n_spheres; i++) if (!mat_ok(s.spheres[i].material)) return bad("sphere material");
     for (uint32_t i = 0; i < s.n_mspheres; i++) if (!mat_ok(s.mspheres[i].material)) return bad("msphere material");
@@ -1165,6 +1244,8 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out) {
             const gs_image& im = s.images[t.image];
             if (!im.width || !im.height) return bad("empty image");
             if (im.offset + (uint64_t)im.width * im.height * 3 > s.n_texels8) return bad("image texels out of range");
+        } else if (t.kind == GS_TEX_NOISE) {
+            if (s.n_noise_perm != 256 || !s.noise_perm) return bad("noise texture without its 256-byte permutation");
         } else if (t.kind != GS_TEX_SOLID) {
             return bad("texture kind");
         }
@@ -1241,7 +1322,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     if (!s || !out) return fail(GS_ERR_ARG, "null argument");
     *out = nullptr;
     uint32_t depth = 1;
-    gs_status v = validate(*s, &depth);
+    bool nested = false;
+    gs_status v = validate(*s, &depth, &nested);
     if (v != GS_OK) return v;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GS_ERR_NO_DEVICE, "no HIP device visible");
@@ -1316,6 +1398,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     size_t o_lref = L.add(s->list_refs, s->n_list_refs * 4);
     size_t o_inst = L.add(s->instances, s->n_instances * sizeof(gs_instance));
     size_t o_media = L.add(s->media, s->n_media * sizeof(gs_medium));
+    size_t o_perm = L.add(s->noise_perm, s->noise_perm ? s->n_noise_perm : 0);
     size_t o_mat = L.add(mats.data(), mats.size() * sizeof(DMaterial));
     size_t o_tex = L.add(s->textures, s->n_textures * sizeof(gs_texture));
     size_t o_img = L.add(s->images, s->n_images * sizeof(gs_image));
@@ -1350,6 +1433,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     d.list_refs = (const uint32_t*)(b + o_lref);
     d.inst = (const gs_instance*)(b + o_inst);
     d.media = (const gs_medium*)(b + o_media);
+    d.noise_perm = (const uint8_t*)(b + o_perm);
     d.mats = (const DMaterial*)(b + o_mat);
     d.texs = (const gs_texture*)(b + o_tex);
     d.images = (const gs_image*)(b + o_img);
@@ -1362,7 +1446,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ds->params = (KParams*)(b + o_params);
     ds->n_nodes = s->n_nodes;
     ds->stack_depth = depth < 1 ? 1 : depth;
-    ds->has_media = s->n_media != 0;
+    ds->feat = (s->n_media != 0 ? GS_FEAT_MEDIA : 0) | (nested ? GS_FEAT_NESTED : 0);
     ds->fast_boxes = true;
     for (uint32_t i = 0; i < s->n_nodes && ds->fast_boxes; i++)
         for (int k = 0; k < 3; k++)
@@ -1391,6 +1475,15 @@ int64_t gs_partition_capacity(const gs_camera* cam, const gs_partition* p) {
     int64_t nt = tx * ty;
     int64_t mine = nt > p->rank ? (nt - p->rank + p->world_size - 1) / p->world_size : 0;
     return mine * p->tile_w * p->tile_h;
+}
+
+static void (*kernel_for(int feat))(KArgs) {
+    switch (feat) {
+        case GS_FEAT_MEDIA: return gs_render_kernel<GS_FEAT_MEDIA>;
+        case GS_FEAT_NESTED: return gs_render_kernel<GS_FEAT_NESTED>;
+        case GS_FEAT_MEDIA | GS_FEAT_NESTED: return gs_render_kernel<GS_FEAT_MEDIA | GS_FEAT_NESTED>;
+        default: return gs_render_kernel<0>;
+    }
 }
 
 gs_status gs_render_tiles_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
@@ -1486,8 +1579,7 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     int per_cu = g_blocks_per_cu;
     if (per_cu <= 0) {
         int occ = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, ds->has_media ? gs_render_kernel<true> : gs_render_kernel<false>, GS_BLOCK, lds));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel_for(ds->feat), GS_BLOCK, lds));
         per_cu = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
     }
     int64_t blocks = (int64_t)cus * per_cu;
@@ -1495,10 +1587,7 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     int64_t max_blocks = ((int64_t)kp.n_items + GS_BLOCK - 1) / GS_BLOCK;
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks < 1) blocks = 1;
-    if (ds->has_media)
-        hipLaunchKernelGGL(gs_render_kernel<true>, dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
-    else
-        hipLaunchKernelGGL(gs_render_kernel<false>, dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
+    hipLaunchKernelGGL(kernel_for(ds->feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
     if (chunk) {
         const unsigned grid = (unsigned)std::min<int64_t>((cap + 255) / 256, 8192);

@@ -31,6 +31,7 @@ struct SpecBuilder {
                 r = std::make_shared<ImageTexture>(im.width, im.height, im.rgb8);
                 break;
             }
+            case GS_TEX_NOISE: r = std::make_shared<NoiseTexture>(t.p[0]); break;
             default: throw std::invalid_argument("unknown texture kind");
         }
         tex[idx] = r;
@@ -235,6 +236,10 @@ gs_status gs_host_write_ppm(const char* path, int32_t width, int32_t height, con
 }
 
 int32_t gs_host_color_byte(double linear) { return color_byte(linear); }
+
+void gs_host_noise_permutation(uint32_t seed, uint8_t* out256) {
+    if (out256) noise_permutation(seed, out256);
+}
 
 int64_t gs_host_bvh_topology(const gs_scene_spec* spec, int32_t* out, int64_t cap) {
     if (!spec) return -1;

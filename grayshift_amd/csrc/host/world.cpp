@@ -201,6 +201,53 @@ uint32_t ImageTexture::flatten(Flattener& f) const {
     return (uint32_t)s;
 }
 
+void noise_permutation(uint32_t seed, uint8_t out[256]) {
+    // PermutationTable::new: a 16-byte XorShift seed, byte 0 = 1, then the seed's
+    // little-endian bytes repeated in words 1..3.
+    uint8_t real[16] = {0};
+    real[0] = 1;
+    for (int i = 1; i < 4; i++)
+        for (int k = 0; k < 4; k++) real[i * 4 + k] = (uint8_t)(seed >> (8 * k));
+    uint32_t x[4];
+    for (int i = 0; i < 4; i++)
+        x[i] = (uint32_t)real[4 * i] | ((uint32_t)real[4 * i + 1] << 8) | ((uint32_t)real[4 * i + 2] << 16) |
+               ((uint32_t)real[4 * i + 3] << 24);
+    auto next_u32 = [&]() {  // rand_xorshift 0.3 XorShiftRng::next_u32
+        const uint32_t t = x[0] ^ (x[0] << 11);
+        x[0] = x[1];
+        x[1] = x[2];
+        x[2] = x[3];
+        x[3] = x[3] ^ (x[3] >> 19) ^ (t ^ (t >> 8));
+        return x[3];
+    };
+    auto gen_index = [&](uint32_t range) {  // rand 0.8 gen_range(0..range) for u32: widening multiply + zone
+        const uint32_t zone = (range << __builtin_clz(range)) - 1u;
+        for (;;) {
+            const uint64_t m = (uint64_t)next_u32() * range;
+            if ((uint32_t)m <= zone) return (uint32_t)(m >> 32);
+        }
+    };
+    for (int i = 0; i < 256; i++) out[i] = (uint8_t)i;
+    for (uint32_t i = 255; i >= 1; i--) {  // SliceRandom::shuffle
+        const uint32_t j = gen_index(i + 1);
+        const uint8_t t = out[i];
+        out[i] = out[j];
+        out[j] = t;
+    }
+}
+
+uint32_t NoiseTexture::flatten(Flattener& f) const {
+    size_t s = slot_of(f.tex_keys, this);
+    if (f.noise_perm.empty()) {
+        f.noise_perm.resize(256);
+        noise_permutation(0, f.noise_perm.data());  // Perlin::DEFAULT_SEED
+    }
+    gs_texture& t = f.textures[s];
+    t.kind = GS_TEX_NOISE;
+    t.color[0] = scale;
+    return (uint32_t)s;
+}
+
 uint32_t Lambertian::flatten(Flattener& f) const {
     size_t s = slot_of(f.mat_keys, this);
     uint32_t tex = f.texture_index(texture.get());
@@ -295,12 +342,13 @@ uint32_t HittableList::flatten(Flattener& f) const {
     return GS_MAKE_REF(GS_REF_LIST, f.lists.size() - 1);
 }
 static uint32_t flatten_instance_child(Flattener& f, const Hittable& o) {
+    if (f.inside_nested_bvh)
+        throw std::domain_error("Translate/RotateY inside a BVH that is itself under Translate/RotateY is not "
+                                "supported on the device path");
     bool was = f.inside_instance;
     f.inside_instance = true;
     uint32_t r = o.flatten(f);
     f.inside_instance = was;
-    uint32_t k = r >> GS_REF_SHIFT;
-    if (k == GS_REF_NODE) throw std::domain_error("BVH under Translate/RotateY is not supported on the device path");
     return r;
 }
 uint32_t Translate::flatten(Flattener& f) const {
@@ -329,17 +377,25 @@ uint32_t RotateY::flatten(Flattener& f) const {
     return GS_MAKE_REF(GS_REF_INSTANCE, idx);
 }
 uint32_t BVHNode::flatten(Flattener& f) const {
-    if (f.inside_instance) throw std::domain_error("BVH under Translate/RotateY is not supported on the device path");
     if (f.inside_medium) throw std::domain_error("BVH as a ConstantMedium boundary is not supported on the device path");
+    // A BVH under Translate/RotateY (final_scene's balls, main.rs:741-755) is walked by the
+    // device as a second-level tree on its own stack: its depth does not count towards
+    // the top-level (LDS) stack.
+    const bool top = !f.inside_instance;
+    const bool was_nested = f.inside_nested_bvh;
+    if (!top) f.inside_nested_bvh = true;
     // Pre-order: the left subtree follows its parent in memory (cache locality).
     size_t idx = f.nodes.size();
     check_index(idx, "nodes");
     f.nodes.push_back(gs_node{});
-    f.depth++;
-    if (f.depth > f.max_depth) f.max_depth = f.depth;
+    if (top) {
+        f.depth++;
+        if (f.depth > f.max_depth) f.max_depth = f.depth;
+    }
     uint32_t l = left->flatten(f);
     uint32_t r = right ? right->flatten(f) : (uint32_t)GS_REF_NONE;
-    f.depth--;
+    if (top) f.depth--;
+    f.inside_nested_bvh = was_nested;
     gs_node& n = f.nodes[idx];
     n.min[0] = bbox.x.min; n.min[1] = bbox.y.min; n.min[2] = bbox.z.min;
     n.max[0] = bbox.x.max; n.max[1] = bbox.y.max; n.max[2] = bbox.z.max;
@@ -351,6 +407,8 @@ uint32_t BVHNode::flatten(Flattener& f) const {
 uint32_t ConstantMedium::flatten(Flattener& f) const {  // volume.rs:10-29
     if (f.inside_medium)
         throw std::domain_error("ConstantMedium inside a ConstantMedium boundary is not supported on the device path");
+    if (f.inside_nested_bvh)
+        throw std::domain_error("ConstantMedium inside a BVH under Translate/RotateY is not supported on the device path");
     size_t idx = f.media.size();
     check_index(idx, "media");
     f.media.push_back(gs_medium{});
@@ -379,6 +437,8 @@ void FlatScene::finalize(uint32_t root, const Background& bg) {
     v.list_refs = f.list_refs.data();   v.n_list_refs = (uint32_t)f.list_refs.size();
     v.instances = f.instances.data();   v.n_instances = (uint32_t)f.instances.size();
     v.media = f.media.data();           v.n_media = (uint32_t)f.media.size();
+    v.noise_perm = f.noise_perm.empty() ? nullptr : f.noise_perm.data();
+    v.n_noise_perm = (uint32_t)f.noise_perm.size();
     v.materials = f.materials.data();   v.n_materials = (uint32_t)f.materials.size();
     v.textures = f.textures.data();     v.n_textures = (uint32_t)f.textures.size();
     v.images = f.images.data();         v.n_images = (uint32_t)f.images.size();

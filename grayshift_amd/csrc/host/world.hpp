@@ -122,6 +122,20 @@ public:
     const uint8_t* rgb8;
 };
 
+// NoiseTexture (texture.rs:97-131): Perlin::default() of the `noise` crate; the device
+// evaluates it from the crate's seed-0 permutation table, which flatten() generates.
+class NoiseTexture : public Texture {
+public:
+    explicit NoiseTexture(double scale) : scale(scale) {}
+    uint32_t flatten(Flattener& f) const override;
+    double scale;
+};
+
+// noise 0.9 PermutationTable::new(seed): XorShiftRng seeded from `seed`, then a rand 0.8
+// Fisher-Yates shuffle of 0..=255.  Restated from the crates' published algorithms
+// (their source is not in this image: parity unpinned).
+void noise_permutation(uint32_t seed, uint8_t out[256]);
+
 // --------------------------------------------------------------- materials
 class Material {
 public:
@@ -311,6 +325,7 @@ public:
     std::vector<uint32_t> list_refs;
     std::vector<gs_instance> instances;
     std::vector<gs_medium> media;
+    std::vector<uint8_t> noise_perm;  // 256 B once any NoiseTexture is flattened
     std::vector<gs_material> materials;
     std::vector<gs_texture> textures;
     std::vector<gs_image> images;
@@ -321,6 +336,7 @@ public:
     uint32_t depth = 0, max_depth = 0;  // BVH node nesting while flattening
     bool inside_instance = false;
     bool inside_medium = false;  // flattening a ConstantMedium boundary
+    bool inside_nested_bvh = false;  // flattening a BVH under Translate/RotateY
 };
 
 // A flattened world + background, ready for gs_render / gs_device_scene_create.

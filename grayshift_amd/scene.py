@@ -73,6 +73,10 @@ class SceneBuilder:
         self._images.append(N.gs_image_spec(width=a.shape[1], height=a.shape[0], rgb8=a.ctypes.data))
         return len(self._images) - 1
 
+    def noise(self, scale):  # NoiseTexture::new (texture.rs:102-104): Perlin::default()
+        self._textures.append(N.gs_texture_spec(kind=N.GS_TEX_NOISE, a=-1, b=-1, p=(scale, 0.0, 0.0)))
+        return len(self._textures) - 1
+
     def image_texture(self, image_index):
         self._textures.append(N.gs_texture_spec(kind=N.GS_TEX_IMAGE, a=image_index, b=-1))
         return len(self._textures) - 1

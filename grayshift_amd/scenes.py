@@ -132,6 +132,64 @@ def earth(width=400, settings=None, hdri=False):
     return Scene("earth_hdr" if hdri else "earth", b.build(), cam, settings or sample_settings(0.95, 0.25, 32, 1000))
 
 
+def perlin_spheres(width=400, settings=None):  # main.rs:255-297
+    b = SceneBuilder()
+    m = b.lambertian_texture(b.noise(4.0))
+    b.add(b.sphere((0.0, -1000.0, 0.0), 1000.0, m))
+    b.add(b.sphere((0.0, 2.0, 0.0), 2.0, m))
+    b.background_solid((0.7, 0.8, 1.0))
+    cam = _camera(16.0 / 9.0, width, 50, 20.0, (13.0, 2.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 0.0, 10.0)
+    return Scene("perlin_spheres", b.build(), cam, settings or sample_settings(0.95, 0.25, 32, 1000))
+
+
+def simple_light(width=1000, settings=None):  # main.rs:366-419
+    b = SceneBuilder()
+    m = b.lambertian_texture(b.noise(4.0))
+    b.add(b.sphere((0.0, -1000.0, 0.0), 1000.0, m))
+    b.add(b.sphere((0.0, 2.0, 0.0), 2.0, m))
+    b.add(b.quad((3.0, 1.0, -2.0), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), b.diffuse_light((4.0, 4.0, 4.0))))
+    b.background_solid((0.0, 0.0, 0.0))
+    cam = _camera(16.0 / 9.0, width, 50, 20.0, (26.0, 3.0, 6.0), (0.0, 2.0, 0.0), (0.0, 1.0, 0.0), 0.0, 10.0)
+    return Scene("simple_light", b.build(), cam, settings or sample_settings(0.95, 0.25, 32, 1000))
+
+
+def final_scene(width=800, settings=None, max_depth=40, boxes_per_side=20, n_balls=1000):
+    """main.rs:626-790 (SCENE 9: width 800, depth 40; SCENE 8: 400, 50).  Everything the
+    reference uses: a BVH of 400 cubes inside the world BVH, a light quad, a moving
+    sphere, glass / metal / earth / noise spheres, two media (a foggy glass sphere and a
+    world fog), and a BVH of 1000 balls under Translate(RotateY).  The scene draws come
+    from one wyrand stream in main.rs's order (box heights, then ball centres)."""
+    rng = Wyrand(SCENE_SEED)
+    b = SceneBuilder()
+    ground = b.lambertian((0.48, 0.83, 0.53))
+    boxes = []
+    for i in range(boxes_per_side):
+        for j in range(boxes_per_side):
+            w = 100.0
+            x0 = -1000.0 + i * w
+            z0 = -1000.0 + j * w
+            y1 = rng.random_f64(1.0, 101.0)
+            boxes.append(b.cube((x0, 0.0, z0), (x0 + w, y1, z0 + w), ground))
+    b.add(b.bvh(boxes))
+    b.add(b.quad((123.0, 554.0, 147.0), (300.0, 0.0, 0.0), (0.0, 0.0, 265.0), b.diffuse_light((7.0, 7.0, 7.0))))
+    c1 = (400.0, 400.0, 200.0)
+    b.add(b.moving_sphere(c1, (c1[0] + 30.0, c1[1], c1[2]), 50.0, b.lambertian((0.7, 0.3, 0.1))))
+    b.add(b.sphere((260.0, 150.0, 45.0), 50.0, b.dielectric(1.5)))
+    b.add(b.sphere((0.0, 150.0, 145.0), 50.0, b.metal((0.8, 0.8, 0.9), 1.0)))
+    b.add(b.sphere((400.0, 200.0, 400.0), 100.0, b.lambertian_texture(b.image_texture(b.image(assets.earthmap_rgb8())))))
+    b.add(b.sphere((220.0, 280.0, 300.0), 80.0, b.lambertian_texture(b.noise(0.2))))
+    fog = b.dielectric(1.5)
+    b.add(b.medium(b.sphere((360.0, 150.0, 145.0), 70.0, fog), 0.2, b.lambertian((0.2, 0.4, 0.9))))
+    b.add(b.medium(b.sphere((0.0, 0.0, 0.0), 5000.0, fog), 0.0001, b.lambertian((1.0, 1.0, 1.0))))
+    white = b.lambertian((0.73, 0.73, 0.73))
+    balls = [b.sphere(rng.random_vector(0.0, 165.0), 10.0, white) for _ in range(n_balls)]
+    b.add(b.translate(b.rotate_y(b.bvh(balls), 15.0), (-100.0, 270.0, 395.0)))
+    b.background_solid((0.0, 0.0, 0.0))
+    cam = _camera(1.0, width, max_depth, 40.0, (478.0, 278.0, -600.0), (278.0, 278.0, 0.0), (0.0, 1.0, 0.0), 0.0,
+                  10.0)
+    return Scene("final_scene", b.build(), cam, settings or sample_settings(0.95, 0.25, 32, 1000))
+
+
 def quads(width=400, settings=None):  # main.rs:299-364
     b = SceneBuilder()
     b.add(b.quad((-3.0, -2.0, 5.0), (0.0, 0.0, -4.0), (0.0, 4.0, 0.0), b.lambertian((1.0, 0.2, 0.2))))
@@ -244,6 +302,9 @@ SCENES = {
     "hdri": hdri,
     "triangles": triangles,
     "mixed": mixed,
+    "perlin_spheres": perlin_spheres,
+    "simple_light": simple_light,
+    "final_scene": final_scene,
 }
 
 # BASELINE.json configs: (builder, kwargs, width, spp)

@@ -131,7 +131,7 @@ typedef struct gs_texture {
     uint32_t kind;      /* gs_tex_kind */
     uint32_t even, odd; /* CHECKERED: texture indices */
     uint32_t image;     /* IMAGE: index into images[] */
-    double color[3];    /* SOLID */
+    double color[3];    /* SOLID; NOISE: color[0] = scale (texture.rs:103) */
     double scale_inv;   /* CHECKERED: 1/scale (texture.rs:42) */
 } gs_texture;
 
@@ -169,6 +169,9 @@ typedef struct gs_flat_scene {
     gs_background background;
     const float* hdri_rgb;        uint64_t n_hdri_floats; /* width*height*3 */
     const gs_medium* media;       uint32_t n_media;       /* (ABI 2) */
+    /* Perlin::default()'s permutation table (noise 0.9 PermutationTable::new(0)): 256
+     * bytes when any texture is NOISE, else NULL / 0 (ABI 3). */
+    const uint8_t* noise_perm;    uint32_t n_noise_perm;
 } gs_flat_scene;
 
 /* The fields `Camera::new` derives (camera.rs:17-98), computed by the host. */

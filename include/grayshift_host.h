@@ -49,6 +49,9 @@ int32_t gs_host_color_byte(double linear);
  * Returns the number of int32 written (or needed when out is NULL), -1 on error. */
 int64_t gs_host_bvh_topology(const gs_scene_spec* spec, int32_t* out, int64_t cap);
 
+/* noise 0.9 PermutationTable::new(seed) as the host generates it for NoiseTexture. */
+void gs_host_noise_permutation(uint32_t seed, uint8_t* out256);
+
 /* sizeof() of a public struct by name ("gs_object", "gs_camera", ...), for FFI
  * mirrors to check their layout; -1 if unknown. */
 int64_t gs_host_struct_size(const char* name);

@@ -60,7 +60,8 @@ typedef struct gs_material_spec {
 enum gs_tex_kind {
     GS_TEX_SOLID     = 1, /* texture.rs:13  p: albedo[3]                               */
     GS_TEX_CHECKERED = 2, /* texture.rs:33  a = even texture, b = odd texture, p[0] = scale */
-    GS_TEX_IMAGE     = 3  /* texture.rs:73  a = image index                            */
+    GS_TEX_IMAGE     = 3, /* texture.rs:73  a = image index                            */
+    GS_TEX_NOISE     = 4  /* texture.rs:97  p[0] = scale; Perlin::default() (noise 0.9) */
 };
 
 typedef struct gs_texture_spec {
@@ -138,7 +139,8 @@ typedef struct gs_counters {
     uint64_t paths;           /* camera samples (get_ray calls)              */
     uint64_t pixels;          /* pixels finished                             */
     uint64_t medium_tests;    /* ConstantMedium::hit           volume.rs:32  */
-    uint64_t reserved[2];
+    uint64_t noise_evals;     /* NoiseTexture::value_at        texture.rs:127 */
+    uint64_t reserved[1];
 } gs_counters;
 
 #ifdef __cplusplus

@@ -240,6 +240,119 @@ struct CheckeredTexture : Texture { /* :33-71 */
         return is_even ? even->value_at(u, v, p) : odd->value_at(u, v, p);
     }
 };
+/* NoiseTexture (texture.rs:97-131) over `noise` 0.9.0's Perlin::default().  The crate
+ * (and rand 0.8 / rand_xorshift 0.3 under it) is not in this image: this restates the
+ * published algorithms — PARITY UNPINNED against the real crate. */
+namespace noise09 {
+struct XorShiftRng { /* rand_xorshift 0.3 */
+    uint32_t x, y, z, w;
+    explicit XorShiftRng(const uint8_t seed[16]) {
+        uint32_t v[4];
+        for (int i = 0; i < 4; i++) std::memcpy(&v[i], seed + 4 * i, 4); /* read_u32_into (LE) */
+        x = v[0]; y = v[1]; z = v[2]; w = v[3];
+    }
+    uint32_t next_u32() {
+        uint32_t t = x ^ (x << 11);
+        x = y; y = z; z = w;
+        w = w ^ (w >> 19) ^ (t ^ (t >> 8));
+        return w;
+    }
+    /* rand 0.8 UniformInt<u32>::sample_single(0, n): Lemire widening multiply, rejection zone */
+    uint32_t gen_range(uint32_t n) {
+        uint32_t range = n;
+        uint32_t zone = (range << __builtin_clz(range)) - 1u;
+        for (;;) {
+            uint64_t m = (uint64_t)next_u32() * (uint64_t)range;
+            uint32_t hi = (uint32_t)(m >> 32), lo = (uint32_t)m;
+            if (lo <= zone) return hi;
+        }
+    }
+};
+struct PermutationTable { /* noise 0.9 permutationtable.rs */
+    uint8_t values[256];
+    explicit PermutationTable(uint32_t seed) {
+        uint8_t real[16] = {0};
+        real[0] = 1;
+        for (int i = 1; i < 4; i++) {
+            real[i * 4] = (uint8_t)seed;
+            real[i * 4 + 1] = (uint8_t)(seed >> 8);
+            real[i * 4 + 2] = (uint8_t)(seed >> 16);
+            real[i * 4 + 3] = (uint8_t)(seed >> 24);
+        }
+        XorShiftRng rng(real);
+        for (int i = 0; i < 256; i++) values[i] = (uint8_t)i;
+        for (int i = 255; i >= 1; i--) std::swap(values[i], values[rng.gen_range((uint32_t)i + 1)]); /* shuffle */
+    }
+    size_t hash(const int64_t* v, int n) const { /* fold: values[a] ^ b, then values[.] */
+        size_t idx = (size_t)(v[0] & 0xff);
+        for (int k = 1; k < n; k++) idx = (size_t)values[idx] ^ (size_t)(v[k] & 0xff);
+        return values[idx];
+    }
+};
+static int64_t numcast_isize(double f) { /* panics in the crate for NaN / out of range; saturate here */
+    if (std::isnan(f)) return 0;
+    if (f >= 9223372036854775808.0) return INT64_MAX;
+    if (f <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)f;
+}
+static double gradient_dot_v(size_t perm, double x, double y, double z) {
+    switch (perm & 0xF) {
+        case 0: return x + y;   case 1: return -x + y;  case 2: return x - y;   case 3: return -x - y;
+        case 4: return x + z;   case 5: return -x + z;  case 6: return x - z;   case 7: return -x - z;
+        case 8: return y + z;   case 9: return -y + z;  case 10: return y - z;  case 11: return -y - z;
+        case 12: return x + y;  case 13: return -x + y; case 14: return -y + z; default: return -y - z;
+    }
+}
+static double s_curve5(double t) { return t * t * t * (t * (t * 6.0 - 15.0) + 10.0); }
+/* core/perlin.rs perlin_3d */
+static double perlin_3d(const double point[3], const PermutationTable& hasher) {
+    const double SCALE_FACTOR = 1.1547005383792515;
+    double floored[3] = {std::floor(point[0]), std::floor(point[1]), std::floor(point[2])};
+    int64_t corner[3] = {numcast_isize(floored[0]), numcast_isize(floored[1]), numcast_isize(floored[2])};
+    double distance[3] = {point[0] - floored[0], point[1] - floored[1], point[2] - floored[2]};
+    auto g = [&](int ox, int oy, int oz) {
+        int64_t c[3] = {corner[0] + ox, corner[1] + oy, corner[2] + oz};
+        return gradient_dot_v(hasher.hash(c, 3), distance[0] - (double)ox, distance[1] - (double)oy,
+                              distance[2] - (double)oz);
+    };
+    double g000 = g(0, 0, 0), g100 = g(1, 0, 0), g010 = g(0, 1, 0), g110 = g(1, 1, 0);
+    double g001 = g(0, 0, 1), g101 = g(1, 0, 1), g011 = g(0, 1, 1), g111 = g(1, 1, 1);
+    double a = s_curve5(distance[0]), b = s_curve5(distance[1]), c = s_curve5(distance[2]);
+    double k0 = g000;
+    double k1 = g100 - g000;
+    double k2 = g010 - g000;
+    double k3 = g001 - g000;
+    double k4 = g000 + g110 - g100 - g010;
+    double k5 = g000 + g101 - g100 - g001;
+    double k6 = g000 + g011 - g010 - g001;
+    double k7 = g100 + g010 + g001 + g111 - g000 - g110 - g101 - g011;
+    double result = k0 + k1 * a + k2 * b + k3 * c + k4 * a * b + k5 * a * c + k6 * b * c + k7 * a * b * c;
+    return result * SCALE_FACTOR;
+}
+} /* namespace noise09 */
+
+struct NoiseTexture : Texture { /* :97-131 */
+    double scale;
+    noise09::PermutationTable noise; /* Perlin::default(): seed 0 */
+    explicit NoiseTexture(double s) : scale(s), noise(0) {}
+    double turbulence(Vec3 p, uint32_t depth) const { /* :107-124 */
+        double accum = 0.0;
+        Vec3 sample_point = p;
+        double weight = 1.0;
+        for (uint32_t i = 0; i < depth; i++) {
+            double pt[3] = {sample_point.x, sample_point.y, sample_point.z};
+            accum += weight * noise09::perlin_3d(pt, noise);
+            weight /= 2.0;
+            sample_point = sample_point * 2.0;
+        }
+        return std::fabs(accum);
+    }
+    Vec3 value_at(double, double, const Vec3& p) const override { /* :127-130 */
+        tl_cnt.noise_evals++;
+        return Vec3(0.5, 0.5, 0.5) * (1.0 + std::sin(scale * p.z + 10.0 * turbulence(p, 7)));
+    }
+};
+
 struct ImageTexture : Texture { /* :73-95 */
     int32_t w, h;
     const uint8_t* rgb;
@@ -895,6 +1008,7 @@ static const Texture* build_texture(const gs_scene_spec& s, int idx, World& w, s
             tex = std::make_unique<ImageTexture>(im.width, im.height, im.rgb8);
             break;
         }
+        case GS_TEX_NOISE: tex = std::make_unique<NoiseTexture>(t.p[0]); break;
         default: throw std::runtime_error("unknown texture kind");
     }
     memo[idx] = tex.get();
@@ -1116,6 +1230,20 @@ int64_t oracle_ppm_text(const uint8_t* rgb8, int32_t w, int32_t h, char* out, in
         t += std::to_string(rgb8[3 * k]) + " " + std::to_string(rgb8[3 * k + 1]) + " " + std::to_string(rgb8[3 * k + 2]) + "\n";
     if (out && cap >= (int64_t)t.size()) std::memcpy(out, t.data(), t.size());
     return (int64_t)t.size();
+}
+/* noise 0.9 Perlin::default() pieces, for KATs: the seed-0 permutation table, one
+ * perlin_3d value, and NoiseTexture::value_at's channel value. */
+void oracle_noise_perm(uint32_t seed, uint8_t* out256) {
+    noise09::PermutationTable t(seed);
+    std::memcpy(out256, t.values, 256);
+}
+double oracle_perlin3(const double* p) {
+    static const noise09::PermutationTable t(0);
+    return noise09::perlin_3d(p, t);
+}
+double oracle_noise_value(double scale, const double* p) {
+    NoiseTexture n(scale);
+    return n.value_at(0.0, 0.0, Vec3(p[0], p[1], p[2])).x;
 }
 /* Checkered texture parity (texture.rs:58-70): returns 1 for even. */
 int oracle_checker_even(double scale, const double* p) {

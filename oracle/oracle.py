@@ -28,6 +28,11 @@ def lib():
         L.oracle_render.argtypes = [C.POINTER(N.gs_scene_spec), C.POINTER(N.gs_camera_spec),
                                     C.POINTER(N.gs_sample_settings), C.c_uint64, C.c_int32, P, C.c_int64, P,
                                     C.POINTER(N.gs_counters), P]
+        L.oracle_noise_perm.argtypes = [C.c_uint32, P]
+        L.oracle_perlin3.restype = C.c_double
+        L.oracle_perlin3.argtypes = [P]
+        L.oracle_noise_value.restype = C.c_double
+        L.oracle_noise_value.argtypes = [C.c_double, P]
         L.oracle_ppm_text.restype = C.c_int64
         L.oracle_ppm_text.argtypes = [P, C.c_int32, C.c_int32, P, C.c_int64]
         L.oracle_camera_fields.argtypes = [C.POINTER(N.gs_camera_spec), P]
@@ -187,3 +192,19 @@ def color_byte(c):
 def checker_even(scale, p):
     pp, ptr = _d(p)
     return bool(lib().oracle_checker_even(scale, ptr))
+
+
+def noise_perm(seed=0):
+    out = np.zeros(256, dtype=np.uint8)
+    lib().oracle_noise_perm(seed, out.ctypes.data)
+    return out
+
+
+def perlin3(p):
+    a, ptr = _d(p)
+    return lib().oracle_perlin3(ptr)
+
+
+def noise_value(scale, p):
+    a, ptr = _d(p)
+    return lib().oracle_noise_value(scale, ptr)

@@ -36,6 +36,10 @@ GOLDEN = {
     "bouncing_adaptive": ("bouncing_spheres", {"grid": 11}, 32, None),
     "cornell_smoke": ("cornell_smoke", {}, 24, 8),
     "smoke_adaptive": ("cornell_smoke", {}, 16, None),
+    "perlin_spheres": ("perlin_spheres", {}, 32, 8),
+    "simple_light": ("simple_light", {}, 32, 8),
+    "final_scene": ("final_scene", {}, 24, 8),
+    "final_adaptive": ("final_scene", {}, 12, None),
 }
 
 

@@ -10,6 +10,7 @@
 
 #include "../../grayshift_amd/csrc/device/devmath.hpp"
 #include "../../grayshift_amd/csrc/device/geometry.hpp"
+#include "../../grayshift_amd/csrc/device/perlin.hpp"
 
 using namespace gsd;
 
@@ -101,6 +102,14 @@ static void back(T* h, T* d, size_t n) {
 }
 static dim3 grid(int n) { return dim3((unsigned)((n + 255) / 256)); }
 
+// perlin3 (which 0) or NoiseTexture's channel value at scale s (which 1) per point.
+__global__ void k_noise(int n, int which, const uint8_t* perm, double scale, const double* p, double* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double* q = p + 3 * i;
+    out[i] = which == 0 ? perlin3(perm, q[0], q[1], q[2]) : noise_value(perm, scale, q[0], q[1], q[2]);
+}
+
 extern "C" {
 
 int kat_aabb(int n, const double* box, const double* ray, const double* iv, int* out) {
@@ -150,6 +159,16 @@ int kat_math(int n, int which, const double* x, const double* y, double* out) {
     hipLaunchKernelGGL(k_math, grid(n), dim3(256), 0, 0, n, which, dx, dy, dout);
     back(out, dout, n);
     (void)hipFree(dx); (void)hipFree(dy);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+int kat_noise(int n, int which, const uint8_t* perm256, double scale, const double* p, double* out) {
+    uint8_t* dperm = dcopy(perm256, 256);
+    double* dp = dcopy(p, 3 * (size_t)n);
+    double* dout = dcopy<double>(nullptr, n);
+    hipLaunchKernelGGL(k_noise, grid(n), dim3(256), 0, 0, n, which, dperm, scale, dp, dout);
+    back(out, dout, n);
+    (void)hipFree(dperm); (void)hipFree(dp);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 

@@ -20,7 +20,8 @@ def kat(built):
     P = C.c_void_p
     for f, args in {"kat_aabb": [C.c_int, P, P, P, P], "kat_sphere": [C.c_int, P, P, P, P, P],
                     "kat_tri": [C.c_int, P, P, P, P], "kat_rng": [C.c_int, P, P, P, C.c_int, P],
-                    "kat_math": [C.c_int, C.c_int, P, P, P]}.items():
+                    "kat_math": [C.c_int, C.c_int, P, P, P],
+                    "kat_noise": [C.c_int, C.c_int, P, C.c_double, P, P]}.items():
         getattr(L, f).argtypes = args
         getattr(L, f).restype = C.c_int
     return L
@@ -131,3 +132,34 @@ def test_transcendentals_within_one_ulp_of_libm(kat, which, fn, lo, hi):
     ulps = np.abs(out - ref) / np.spacing(np.abs(ref))
     assert ulps.max() <= 1.0
     print("which=%d mismatch rate %.4f" % (which, float((out != ref).mean())))
+
+
+def test_perlin_matches_oracle_bitwise(kat):
+    """NoiseTexture's Perlin (noise 0.9 restated, perlin.hpp) against the oracle's
+    independent restatement: bit-identical (pure f64 + - * and floor)."""
+    rng = np.random.default_rng(11)
+    n = 20000
+    p = rng.uniform(-300, 300, (n, 3))
+    p[: n // 10] = np.round(p[: n // 10])          # lattice points (exactly 0)
+    p[n // 10: n // 5] *= 1e-3                      # near the origin, both signs
+    p = np.ascontiguousarray(p)
+    perm = np.ascontiguousarray(oracle.noise_perm(0))
+    out = np.zeros(n)
+    assert kat.kat_noise(n, 0, ptr(perm), 0.0, ptr(p), ptr(out)) == 0
+    ref = np.array([oracle.perlin3(q) for q in p])
+    assert np.array_equal(out, ref)
+    assert (out[: n // 10] == 0.0).all()
+
+
+def test_noise_texture_value_within_libm_ulps(kat):
+    """value_at = 0.5 * (1 + sin(scale * z + 10 * turbulence)): turbulence is bit-exact,
+    sin is OCML vs glibc (<= 1 ulp), so the channel differs by at most a few ulps."""
+    rng = np.random.default_rng(12)
+    n = 5000
+    p = np.ascontiguousarray(rng.uniform(-400, 600, (n, 3)))
+    perm = np.ascontiguousarray(oracle.noise_perm(0))
+    for scale in (4.0, 0.2):
+        out = np.zeros(n)
+        assert kat.kat_noise(n, 1, ptr(perm), scale, ptr(p), ptr(out)) == 0
+        ref = np.array([oracle.noise_value(scale, q) for q in p])
+        assert np.abs(out - ref).max() <= 4 * np.spacing(1.0)

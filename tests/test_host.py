@@ -200,11 +200,30 @@ def test_unsupported_media_are_rejected(case):
     assert N.lib.gs_host_scene_from_spec(b.build().ptr(), C.byref(h)) == N.GS_ERR_UNSUPPORTED
 
 
-def test_bvh_under_instance_is_unsupported():
+def test_bvh_under_instance_flattens_as_a_second_level_tree():
+    """final_scene's Translate(RotateY(BVHNode::from_list(balls))) (main.rs:741-755): the
+    inner tree's nodes are flattened but do not count towards the top-level depth."""
     b = SceneBuilder()
     m = b.lambertian((1, 1, 1))
-    inner = b.bvh([b.sphere((0, 0, 0), 1, m), b.sphere((3, 0, 0), 1, m), b.sphere((6, 0, 0), 1, m)])
-    b.add(b.translate(inner, (1, 0, 0)))
+    inner = b.bvh([b.sphere((float(i), 0, 0), 0.4, m) for i in range(40)])
+    b.add(b.translate(b.rotate_y(inner, 15.0), (1, 0, 0)))
+    b.add(b.sphere((0, -100, 0), 99, m))
+    hs = g.HostScene(b.build())
+    st = hs.stats()
+    assert st["instances"] == 2 and st["spheres"] == 41
+    assert st["nodes"] > 1 + 19  # top-level root + the inner tree (>= n/2 nodes for n leaves)
+    assert st["max_bvh_depth"] == 1
+    hs.close()
+
+
+@pytest.mark.parametrize("case", ["instance_in_nested", "medium_in_nested"])
+def test_unsupported_nested_bvh_leaves(case):
+    b = SceneBuilder()
+    m = b.lambertian((1, 1, 1))
+    s1 = b.sphere((0, 0, 0), 1, m)
+    odd = b.translate(b.sphere((3, 0, 0), 1, m), (0, 1, 0)) if case == "instance_in_nested" else \
+        b.medium(b.sphere((3, 0, 0), 1, m), 0.5, m)
+    b.add(b.translate(b.bvh([s1, odd, b.sphere((6, 0, 0), 1, m)]), (1, 0, 0)))
     h = C.c_void_p()
     assert N.lib.gs_host_scene_from_spec(b.build().ptr(), C.byref(h)) == N.GS_ERR_UNSUPPORTED
 

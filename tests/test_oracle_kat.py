@@ -254,3 +254,44 @@ def test_bvh_n3_median_split():
 def test_bvh_depth_is_logarithmic():
     t = _pairs(oracle.bvh_topology(_world(1000)).tolist())
     assert max(d for k, d in t) <= 11  # ceil(log2(1000)) + 1
+
+
+# ------------------------------------------------------ NoiseTexture (noise 0.9)
+def test_noise_permutation_is_a_permutation_and_host_agrees():
+    """PermutationTable::new(0) restated twice (oracle, product host): the same table, a
+    permutation of 0..=255.  Parity with the real crate is unpinned."""
+    import ctypes as C
+    from grayshift_amd import _native as N
+    for seed in (0, 1, 0xDEADBEEF):
+        p = oracle.noise_perm(seed)
+        assert sorted(p.tolist()) == list(range(256))
+        h = np.zeros(256, dtype=np.uint8)
+        N.lib.gs_host_noise_permutation(seed, h.ctypes.data)
+        assert np.array_equal(h, p)
+    assert not np.array_equal(oracle.noise_perm(0), oracle.noise_perm(1))
+
+
+def test_perlin_known_properties():
+    # zero on the integer lattice; continuous across cell faces; bounded
+    for q in [(0, 0, 0), (3, -7, 12), (-1, -1, -1), (255, 256, 257)]:
+        assert oracle.perlin3(np.array(q, float)) == 0.0
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        c = np.floor(rng.uniform(-20, 20, 3))
+        axis = rng.integers(0, 3)
+        a, b = c.copy(), c.copy()
+        a[axis] -= 1e-9
+        b[axis] += 1e-9
+        a += rng.uniform(0.1, 0.9, 3) * (np.arange(3) != axis)
+        b = a.copy()
+        b[axis] = c[axis] + 1e-9
+        assert abs(oracle.perlin3(a) - oracle.perlin3(b)) < 1e-6
+    v = [oracle.perlin3(rng.uniform(-100, 100, 3)) for _ in range(5000)]
+    assert max(abs(x) for x in v) < 1.2 and np.std(v) > 0.1
+
+
+def test_noise_texture_value_formula():
+    # texture.rs:127-130 at a lattice point where every octave is 0: 0.5 * (1 + sin(scale*z))
+    for scale, z in [(4.0, 3.0), (0.2, -8.0)]:
+        p = np.array([5.0, -2.0, z])
+        assert oracle.noise_value(scale, p) == 0.5 * (1.0 + math.sin(scale * z))
