@@ -1062,7 +1062,12 @@ static thread_local std::string tl_err;
 static int32_t g_shade_batch = 52;  // swept on MI355X C4 (chunked, uniform loop): 48 -> 3502, 52 -> 3535-3568, 56 -> 3506-3536 Msamples/s
 static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
 static int32_t g_leaf_batch = 8;
-static int32_t g_sample_chunk = -1;  // -1 auto, 0 never split a pixel's samples  // swept on MI355X C4: 0 -> 1940, 8 -> 1986, 16 -> 1923, 32 -> 1770 Msamples/s
+// -1 auto, 0 never split a pixel's samples.  Swept on MI355X, C4 rank 0 of N
+// (tools/rank_sim.py; ms): N=1: 32 -> 808.7, 16 -> 803.2, 8 -> 804.9, 4 -> 805.2;
+// N=8: 32 -> 113.3, 16 -> 110.2, 8 -> 107.4, 4 -> 107.5.  Small chunks cost nothing at
+// one GPU and shorten the queue's tail when a rank holds few pixels per lane.
+static int32_t g_sample_chunk = -1;
+static const uint64_t kPartialBudget = 4ull << 30;  // auto chunks: at most 4 GiB of chunk sums
 
 extern "C" void gs_set_last_error(const char* msg) { tl_err = msg ? msg : ""; }
 static gs_status fail(gs_status code, const std::string& msg) {
@@ -1533,8 +1538,10 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     uint32_t chunk = 0, cpp = 1;
     if (g_sample_chunk != 0 && ss->max_samples < ss->batch_size) {
         const uint32_t bs = ss->batch_size;
-        uint32_t c = g_sample_chunk > 0 ? (uint32_t)g_sample_chunk : std::max<uint32_t>(32u, (bs + 31u) / 32u);
+        uint32_t c = g_sample_chunk > 0 ? (uint32_t)g_sample_chunk : std::max<uint32_t>(8u, (bs + 63u) / 64u);
         if ((bs + c - 1) / c > 64u) c = (bs + 63u) / 64u;  // at most 64 chunks per pixel
+        if (g_sample_chunk < 0)
+            while (c < bs && (uint64_t)cap * ((bs + c - 1) / c) * 24u > kPartialBudget) c *= 2u;
         if (c < bs) {
             chunk = c;
             cpp = (bs + c - 1) / c;

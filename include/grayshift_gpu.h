@@ -208,8 +208,9 @@ int32_t gs_version(void);
  * occupancy query; leaf_batch in [0, 64] = lanes waiting at a leaf before the wave
  * runs a leaf-test pass (0 acts as 1);
  * sample_chunk = samples per work item when the settings run a single batch
- * (max_samples < batch_size, as every fixed-spp render): -1 auto (32, or batch/32 for
- * big batches, at most 64 chunks per pixel), 0 never split a pixel, n > 0 explicit.
+ * (max_samples < batch_size, as every fixed-spp render): -1 auto (8, or batch/64 for
+ * big batches: at most 64 chunks per pixel, and at most 4 GiB of chunk sums), 0 never
+ * split a pixel, n > 0 explicit.
  * Chunks keep every sample's RNG stream; a pixel's chunk sums are added in sample order,
  * so only the association of the f64 colour sum differs from the sequential loop. */
 gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf_batch, int32_t sample_chunk);
