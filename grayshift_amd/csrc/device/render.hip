@@ -151,6 +151,31 @@ __host__ __device__ inline uint32_t device_ref(uint32_t abi_ref) {
     return abi_ref;
 }
 
+// Threaded top-level tree (the default walk; -DGS_STACK_WALK keeps the LDS-stack walk).
+// BVHNode::hit's left-first recursion (BVH.rs:69-90) visits the tree in pre-order, and a
+// box miss skips exactly the node's subtree.  So the top-level tree is stored as its
+// pre-order sequence of records — one per node AND one per leaf occurrence — where a node
+// record holds its box, a hit link (the next record: its left child) and a miss link (the
+// record after its subtree), and a leaf record holds the primitive's ABI ref, a stationary
+// sphere's centre/radius inline, and its next link.  The walk is then `cur = hit ? hit_link
+// : miss_link` with no stack: the same records tested in the same order with the same
+// closest t, minus every push, pop and LDS stack slot.  Links are record indices, a leaf's
+// tagged with THR_LEAF; THR_END ends the walk.
+#define THR_END 0x7FFFFFFFu
+#define THR_LEAF 0x80000000u
+
+__device__ __forceinline__ void load_leaf_rec(const DNode* p, double& cx, double& cy, double& cz, double& r,
+                                              uint32_t& next, uint32_t& ref) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const uint4 a = q[0], b = q[1], d = q[3];
+    cx = __hiloint2double((int)a.y, (int)a.x);
+    cy = __hiloint2double((int)a.w, (int)a.z);
+    cz = __hiloint2double((int)b.y, (int)b.x);
+    r = __hiloint2double((int)b.w, (int)b.z);
+    next = d.x;
+    ref = d.z;
+}
+
 // Outcome of testing one non-node child against the ray.
 struct LeafHit {
     bool hit;
@@ -593,7 +618,11 @@ enum { L_CSR = 0, L_CSG, L_CSB, L_LSUM, L_LSQ, L_SCOUNT, L_ND };
 enum { L_ITEM = 0, L_PIX, L_BLEFT, L_NI };
 
 __host__ __device__ inline size_t lds_bytes(uint32_t stack_depth) {
+#ifdef GS_STACK_WALK
     return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4 + (stack_depth + 1) * 4);  // + the dummy slot 0
+#else
+    return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4);  // the threaded walk keeps no stack
+#endif
 }
 
 template <int FEAT>
@@ -859,8 +888,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             // do), then test those leaves together, so a wave pays for the node step and the
             // sphere test in different iterations instead of both in every one.  Each lane
             // still processes its refs in the reference's order.  The pass kind is uniform.
+#ifdef GS_STACK_WALK
             const bool at_leaf = tracing && cur >= DREF_LEAF;
             const uint64_t lm = tr & __builtin_amdgcn_ballot_w64(cur >= DREF_LEAF);  // == ballot(at_leaf)
+#else
+            const bool at_leaf = tracing && cur > THR_END;
+            const uint64_t lm = tr & __builtin_amdgcn_ballot_w64(cur > THR_END);  // == ballot(at_leaf)
+#endif
             const bool leaf_pass = lm == tr || (uint32_t)__popcll(lm) >= (uint32_t)A.leaf_batch;
 #ifdef GS_STAMPS
             it_all++;
@@ -869,6 +903,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             ln_node += leaf_pass ? 0ull : (uint64_t)__popcll(tr & ~lm);
             ln_leaf += leaf_pass ? (uint64_t)__popcll(lm) : 0ull;
 #endif
+#ifdef GS_STACK_WALK
             if (!leaf_pass) {
                 if (tracing && !at_leaf) {
                     // All 64 B in one go (4 x dwordx4) and a branchless push: the child refs
@@ -915,6 +950,45 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             cur = pop ? top : cur;
             sp -= pop ? 1u : 0u;
             st = (empty && !pop) ? (uint32_t)S_SHADE : st;
+#else
+            if (!leaf_pass) {
+                if (tracing && !at_leaf) {
+                    // One 64-B record (4 x dwordx4 off the SGPR base, offset = cur << 6), the
+                    // box test, and the next record: the hit link or the miss link.
+                    const DNode nd = load_node((const DNode*)((const char*)A.nodes + (cur << 6)));
+                    c_nodes++;
+                    bool h;
+                    if (wave_fast) {
+                        h = box_hit_fast(nd, ray.o, inv, tmin, closest);
+                    } else {
+                        h = box_hit(nd, ray.o, inv, tmin, closest);
+                    }
+                    cur = h ? nd.left : nd.right;
+                }
+            } else if (at_leaf) {
+                double scx, scy, scz, sr;
+                uint32_t next, ref;
+                load_leaf_rec((const DNode*)((const char*)A.nodes + (cur << 6)), scx, scy, scz, sr, next, ref);
+                if ((ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {  // a stationary sphere, inline
+                    c_sph++;
+                    double t;
+                    if (sphere_accept(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
+                        closest = t;
+                        hit_ref = ref;
+                        hit_inst = GS_REF_NONE;
+                    }
+                } else {
+                    const LeafHit lh = leaf_other<FEAT>(sc, ref, ray, tmin, closest, rng, s_cnt);
+                    if (lh.hit) {
+                        closest = lh.t;
+                        hit_ref = lh.ref;
+                        hit_inst = lh.inst;
+                    }
+                }
+                cur = next;
+            }
+            st = (tracing && cur == THR_END) ? (uint32_t)S_SHADE : st;
+#endif
         }
 
         // ---------------------------------------------------------- shade
@@ -1091,6 +1165,8 @@ struct gs_device_scene {
     uint32_t stack_depth = 1;  // LDS stack entries per lane (= BVH depth)
     bool fast_boxes = false;  // every node coordinate |x| < 1e300
     int feat = 0;             // GS_FEAT_* of the kernel instantiation to launch
+    const DNode* thr = nullptr;  // threaded top-level records (THR_END)
+    uint32_t thr_root = THR_END;
     double* partial = nullptr;  // chunk partial sums, grown on demand
     size_t partial_bytes = 0;
 };
@@ -1339,6 +1415,53 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         nodes[i] = DNode{n.min[0], n.min[1], n.min[2], n.max[0], n.max[1], n.max[2],
                          device_ref(n.left), device_ref(n.right), 0, 0};
     }
+    // The threaded top-level tree (see THR_END): pre-order records of nodes and leaf
+    // occurrences; raw links first, tagged once every record's kind is known.
+    std::vector<DNode> thr;
+    std::vector<uint8_t> thr_leaf;
+    {
+        // Iterative pre-order: a node pushes a "close" marker below its children, which
+        // sets its miss link once its subtree is emitted.
+        std::vector<std::pair<uint32_t, bool>> work{{s->root, false}};
+        while (!work.empty()) {
+            auto [x, close] = work.back();
+            work.pop_back();
+            if (close) {  // x = record index of a node whose subtree is now complete
+                thr[x].right = (uint32_t)thr.size();
+                continue;
+            }
+            const uint32_t idx = (uint32_t)thr.size();
+            DNode rec{};
+            if ((x >> GS_REF_SHIFT) == GS_REF_NODE) {
+                const gs_node& n = s->nodes[x & GS_REF_MASK];
+                rec = DNode{n.min[0], n.min[1], n.min[2], n.max[0], n.max[1], n.max[2], idx + 1u, 0u, 0u, 0u};
+                thr.push_back(rec);
+                thr_leaf.push_back(0);
+                work.push_back({idx, true});
+                if (n.right != GS_REF_NONE) work.push_back({n.right, false});
+                work.push_back({n.left, false});
+            } else {
+                if ((x >> GS_REF_SHIFT) == GS_REF_SPHERE) {
+                    const gs_sphere& q = s->spheres[x & GS_REF_MASK];
+                    rec.mnx = q.center[0];
+                    rec.mny = q.center[1];
+                    rec.mnz = q.center[2];
+                    rec.mxx = q.radius;
+                }
+                rec.left = idx + 1u;  // next
+                rec.pad0 = x;         // the primitive's ABI ref
+                thr.push_back(rec);
+                thr_leaf.push_back(1);
+            }
+        }
+        const uint32_t n = (uint32_t)thr.size();
+        auto tag = [&](uint32_t l) { return l >= n ? THR_END : (thr_leaf[l] ? (THR_LEAF | l) : l); };
+        for (uint32_t i = 0; i < n; i++) {
+            thr[i].left = tag(thr[i].left);
+            if (!thr_leaf[i]) thr[i].right = tag(thr[i].right);
+        }
+    }
+    if (thr.size() >= (1u << 26)) return fail(GS_ERR_UNSUPPORTED, "more than 2^26 top-level BVH records");
     std::vector<DSphere> sph(s->n_spheres);
     std::vector<uint32_t> sph_mat(s->n_spheres);
     for (uint32_t i = 0; i < s->n_spheres; i++) {
@@ -1394,6 +1517,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     }
     Layout L;
     size_t o_nodes = L.add(nodes.data(), nodes.size() * sizeof(DNode));
+    size_t o_thr = L.add(thr.data(), thr.size() * sizeof(DNode));
     size_t o_sph = L.add(sph.data(), sph.size() * sizeof(DSphere));
     size_t o_sphm = L.add(sph_mat.data(), sph_mat.size() * 4);
     size_t o_msph = L.add(s->mspheres, s->n_mspheres * sizeof(gs_msphere));
@@ -1450,6 +1574,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ds->queue = (uint32_t*)(b + o_queue);
     ds->params = (KParams*)(b + o_params);
     ds->n_nodes = s->n_nodes;
+    ds->thr = (const DNode*)(b + o_thr);
+    ds->thr_root = thr.empty() ? THR_END : (thr_leaf[0] ? THR_LEAF : 0u);
     ds->stack_depth = depth < 1 ? 1 : depth;
     ds->feat = (s->n_media != 0 ? GS_FEAT_MEDIA : 0) | (nested ? GS_FEAT_NESTED : 0);
     ds->fast_boxes = true;
@@ -1570,10 +1696,18 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     kp.queue = ds->queue;
     kp.item_visits = outs->item_visits;
     KArgs a{};
+#ifdef GS_STACK_WALK
     a.nodes = ds->dev.nodes;
+#else
+    a.nodes = ds->thr;
+#endif
     a.spheres = ds->dev.spheres;
     a.P = ds->params;
+#ifdef GS_STACK_WALK
     a.root = ds->dev.root;
+#else
+    a.root = ds->thr_root;
+#endif
     a.fast_boxes = ds->fast_boxes ? 1 : 0;
     a.shade_batch = g_shade_batch;
     a.leaf_batch = g_leaf_batch < 1 ? 1 : g_leaf_batch;  // 0 would never step a node
