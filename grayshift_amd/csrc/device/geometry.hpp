@@ -37,6 +37,26 @@ __device__ __forceinline__ DNode load_node(const DNode* p) {
     return n;
 }
 
+// The box and the two links only (56 B: 3 x dwordx4 + dwordx2): the vector-memory pipe,
+// not the bytes, limits the traversal loop, so the pad word is not fetched.
+__device__ __forceinline__ DNode load_node56(const DNode* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const uint4 a = q[0], b = q[1], c = q[2];
+    const uint2 d = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(p) + 48);
+    DNode n;
+    n.mnx = __hiloint2double((int)a.y, (int)a.x);
+    n.mny = __hiloint2double((int)a.w, (int)a.z);
+    n.mnz = __hiloint2double((int)b.y, (int)b.x);
+    n.mxx = __hiloint2double((int)b.w, (int)b.z);
+    n.mxy = __hiloint2double((int)c.y, (int)c.x);
+    n.mxz = __hiloint2double((int)c.w, (int)c.z);
+    n.left = d.x;
+    n.right = d.y;
+    n.pad0 = 0;
+    n.pad1 = 0;
+    return n;
+}
+
 // AABB::hit (AABB.rs:58-113) with the reference's 1.0/d hoisted per ray (same value).
 // The early-outs of the reference do not change the boolean: once max <= min the
 // later slabs only raise min / lower max, and NaN slabs never assign.

@@ -167,13 +167,14 @@ __host__ __device__ inline uint32_t device_ref(uint32_t abi_ref) {
 __device__ __forceinline__ void load_leaf_rec(const DNode* p, double& cx, double& cy, double& cz, double& r,
                                               uint32_t& next, uint32_t& ref) {
     const uint4* q = reinterpret_cast<const uint4*>(p);
-    const uint4 a = q[0], b = q[1], d = q[3];
+    const uint4 a = q[0], b = q[1];
+    const uint2 d = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(p) + 48);
     cx = __hiloint2double((int)a.y, (int)a.x);
     cy = __hiloint2double((int)a.w, (int)a.z);
     cz = __hiloint2double((int)b.y, (int)b.x);
     r = __hiloint2double((int)b.w, (int)b.z);
     next = d.x;
-    ref = d.z;
+    ref = d.y;
 }
 
 // Outcome of testing one non-node child against the ray.
@@ -955,7 +956,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 if (tracing && !at_leaf) {
                     // One 64-B record (4 x dwordx4 off the SGPR base, offset = cur << 6), the
                     // box test, and the next record: the hit link or the miss link.
-                    const DNode nd = load_node((const DNode*)((const char*)A.nodes + (cur << 6)));
+                    const DNode nd = load_node56((const DNode*)((const char*)A.nodes + (cur << 6)));
                     c_nodes++;
                     bool h;
                     if (wave_fast) {
@@ -1449,7 +1450,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                     rec.mxx = q.radius;
                 }
                 rec.left = idx + 1u;  // next
-                rec.pad0 = x;         // the primitive's ABI ref
+                rec.right = x;        // the primitive's ABI ref
                 thr.push_back(rec);
                 thr_leaf.push_back(1);
             }
@@ -1458,7 +1459,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         auto tag = [&](uint32_t l) { return l >= n ? THR_END : (thr_leaf[l] ? (THR_LEAF | l) : l); };
         for (uint32_t i = 0; i < n; i++) {
             thr[i].left = tag(thr[i].left);
-            if (!thr_leaf[i]) thr[i].right = tag(thr[i].right);
+            if (!thr_leaf[i]) thr[i].right = tag(thr[i].right);  // a leaf's `right` is its ref
         }
     }
     if (thr.size() >= (1u << 26)) return fail(GS_ERR_UNSUPPORTED, "more than 2^26 top-level BVH records");
