@@ -38,7 +38,12 @@
 
 using namespace gsd;
 
-#define GS_BLOCK 256
+// One 1024-lane block per CU (4 waves/SIMD): the block's LDS holds the lane state and
+// the largest mirror of the tree's top records (1456 of them; measured on MI355X C4:
+// 256-lane blocks with 352 mirrored records 4060, 1024-lane blocks 4150 Msamples/s).
+#ifndef GS_BLOCK
+#define GS_BLOCK 1024
+#endif
 #define GS_STACK 32  // max BVH depth the device accepts
 // Measured on MI355X (C4): everything inlined with a 4-waves/SIMD register cap (128
 // VGPRs; spills only in shading) beats out-of-line shading calls and 3 or 5 waves.
@@ -135,6 +140,7 @@ struct KArgs {
     int32_t shade_batch;
     int32_t leaf_batch;  // >= 1: tracing lanes at a leaf before a wave runs a leaf pass
     int32_t fast_boxes;  // every node coordinate |x| < 1e300: rays may take box_hit_fast
+    uint32_t lds_top;    // threaded records [0, lds_top) are mirrored in each block's LDS
 };
 
 enum { S_NEED = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };
@@ -173,6 +179,44 @@ __device__ __forceinline__ void load_leaf_rec(const DNode* p, double& cx, double
     cy = __hiloint2double((int)a.w, (int)a.z);
     cz = __hiloint2double((int)b.y, (int)b.x);
     r = __hiloint2double((int)b.w, (int)b.z);
+    next = d.x;
+    ref = d.y;
+}
+
+// The same two loads from the LDS mirror.  Address-space-qualified pointers keep them
+// ds_read instructions: a select between an LDS and a global pointer would compile to
+// flat loads, which measured 34% slower on the whole kernel.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
+typedef __attribute__((address_space(3))) const u32x2 lds_u32x2;
+__device__ __forceinline__ double lo_hi(unsigned int lo, unsigned int hi) { return __hiloint2double((int)hi, (int)lo); }
+__device__ __forceinline__ DNode load_node56_lds(const uint8_t* p) {
+    lds_u32x4* q = (lds_u32x4*)(p);
+    const u32x4 a = q[0], b = q[1], c = q[2];
+    const u32x2 d = *(lds_u32x2*)(p + 48);
+    DNode n;
+    n.mnx = lo_hi(a.x, a.y);
+    n.mny = lo_hi(a.z, a.w);
+    n.mnz = lo_hi(b.x, b.y);
+    n.mxx = lo_hi(b.z, b.w);
+    n.mxy = lo_hi(c.x, c.y);
+    n.mxz = lo_hi(c.z, c.w);
+    n.left = d.x;
+    n.right = d.y;
+    n.pad0 = 0;
+    n.pad1 = 0;
+    return n;
+}
+__device__ __forceinline__ void load_leaf_rec_lds(const uint8_t* p, double& cx, double& cy, double& cz, double& r,
+                                                  uint32_t& next, uint32_t& ref) {
+    lds_u32x4* q = (lds_u32x4*)(p);
+    const u32x4 a = q[0], b = q[1];
+    const u32x2 d = *(lds_u32x2*)(p + 48);
+    cx = lo_hi(a.x, a.y);
+    cy = lo_hi(a.z, a.w);
+    cz = lo_hi(b.x, b.y);
+    r = lo_hi(b.z, b.w);
     next = d.x;
     ref = d.y;
 }
@@ -637,6 +681,17 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     double* s_d = (double*)smem;                                  // [L_ND][GS_BLOCK]
     uint32_t* s_i = (uint32_t*)(smem + L_ND * 8 * GS_BLOCK);      // [L_NI][GS_BLOCK]
     uint32_t* s_stack = s_i + L_NI * GS_BLOCK;                    // [depth][GS_BLOCK]
+#ifndef GS_STACK_WALK
+    // The hottest threaded records (the tree's top levels, placed first by the host) are
+    // mirrored in LDS: a node step then reads them through a flat pointer that resolves to
+    // LDS for those records and to global memory for the rest, per lane.
+    uint8_t* s_top = smem + lds_bytes(0);
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(A.nodes);
+        uint4* dst = reinterpret_cast<uint4*>(s_top);
+        for (uint32_t k = threadIdx.x; k < A.lds_top * 4u; k += GS_BLOCK) dst[k] = src[k];
+    }
+#endif
     if (threadIdx.x < C_N) s_cnt[threadIdx.x] = 0;
     __syncthreads();
 
@@ -956,7 +1011,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 if (tracing && !at_leaf) {
                     // One 64-B record (4 x dwordx4 off the SGPR base, offset = cur << 6), the
                     // box test, and the next record: the hit link or the miss link.
-                    const DNode nd = load_node56((const DNode*)((const char*)A.nodes + (cur << 6)));
+                    DNode nd;
+                    if (cur < A.lds_top) {
+                        nd = load_node56_lds(s_top + (cur << 6));
+                    } else {
+                        nd = load_node56((const DNode*)((const char*)A.nodes + (cur << 6)));
+                    }
                     c_nodes++;
                     bool h;
                     if (wave_fast) {
@@ -969,7 +1029,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             } else if (at_leaf) {
                 double scx, scy, scz, sr;
                 uint32_t next, ref;
-                load_leaf_rec((const DNode*)((const char*)A.nodes + (cur << 6)), scx, scy, scz, sr, next, ref);
+                const uint32_t li = cur & ~THR_LEAF;
+                if (li < A.lds_top) {
+                    load_leaf_rec_lds(s_top + (li << 6), scx, scy, scz, sr, next, ref);
+                } else {
+                    load_leaf_rec((const DNode*)((const char*)A.nodes + (li << 6)), scx, scy, scz, sr, next, ref);
+                }
                 if ((ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {  // a stationary sphere, inline
                     c_sph++;
                     double t;
@@ -1137,6 +1202,18 @@ static thread_local std::string tl_err;
 static int32_t g_shade_batch = 52;  // swept on MI355X C4 (chunked, uniform loop): 48 -> 3502, 52 -> 3535-3568, 56 -> 3506-3536 Msamples/s
 static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
 static int32_t g_leaf_batch = 8;
+// Threaded records mirrored in LDS per block (the shallowest ones): what is left of the
+// block's share of the CU's 160 KiB (4 waves/SIMD = 1024 lanes per CU) after the lane
+// state.  256-lane blocks: 352 records.  -1 = that budget; >= 0 explicit (A/B).
+#ifndef GS_LDS_TOP
+#define GS_LDS_TOP -1
+#endif
+static int32_t g_lds_top = GS_LDS_TOP;
+static uint32_t lds_top_budget() {
+    const int64_t share = (int64_t)160 * 1024 * GS_BLOCK / 1024;
+    const int64_t left = share - (int64_t)GS_BLOCK * (L_ND * 8 + L_NI * 4) - 1024;  // 1 KiB: static LDS + slack
+    return left > 0 ? (uint32_t)(left / 64) : 0u;
+}
 // -1 auto, 0 never split a pixel's samples.  Swept on MI355X, C4 rank 0 of N
 // (tools/rank_sim.py; ms): N=1: 32 -> 808.7, 16 -> 803.2, 8 -> 804.9, 4 -> 805.2;
 // N=8: 32 -> 113.3, 16 -> 110.2, 8 -> 107.4, 4 -> 107.5.  Small chunks cost nothing at
@@ -1168,6 +1245,7 @@ struct gs_device_scene {
     int feat = 0;             // GS_FEAT_* of the kernel instantiation to launch
     const DNode* thr = nullptr;  // threaded top-level records (THR_END)
     uint32_t thr_root = THR_END;
+    uint32_t lds_top = 0;        // records mirrored in LDS per block
     double* partial = nullptr;  // chunk partial sums, grown on demand
     size_t partial_bytes = 0;
 };
@@ -1420,6 +1498,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     // occurrences; raw links first, tagged once every record's kind is known.
     std::vector<DNode> thr;
     std::vector<uint8_t> thr_leaf;
+    uint32_t lds_top = 0, thr_root_tagged = THR_END;
     {
         // Iterative pre-order: a node pushes a "close" marker below its children, which
         // sets its miss link once its subtree is emitted.
@@ -1456,11 +1535,43 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             }
         }
         const uint32_t n = (uint32_t)thr.size();
-        auto tag = [&](uint32_t l) { return l >= n ? THR_END : (thr_leaf[l] ? (THR_LEAF | l) : l); };
-        for (uint32_t i = 0; i < n; i++) {
-            thr[i].left = tag(thr[i].left);
-            if (!thr_leaf[i]) thr[i].right = tag(thr[i].right);  // a leaf's `right` is its ref
+        // Placement: the g_lds_top shallowest records (BFS order: every ray visits the top
+        // levels) first, so a block can mirror them in LDS; the rest in pre-order.  Links
+        // are explicit, so placement does not change the walk.
+        std::vector<uint32_t> pos(n);
+        {
+            std::vector<uint32_t> depth(n, 0), order;
+            for (uint32_t i = 0; i < n; i++)
+                if (!thr_leaf[i]) {
+                    if (thr[i].left < n) depth[thr[i].left] = depth[i] + 1;  // records are pre-order:
+                    // a node's descendants follow it, so depths propagate in one forward pass
+                    for (uint32_t c = thr[i].left; c < thr[i].right && c < n;) {
+                        depth[c] = depth[i] + 1;
+                        c = thr_leaf[c] ? c + 1 : thr[c].right;  // next child of node i
+                    }
+                }
+            order.resize(n);
+            for (uint32_t i = 0; i < n; i++) order[i] = i;
+            const uint32_t k = std::min<uint32_t>(n, g_lds_top < 0 ? lds_top_budget() : (uint32_t)g_lds_top);
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return depth[a] < depth[b]; });
+            std::vector<uint8_t> top(n, 0);
+            for (uint32_t i = 0; i < k; i++) top[order[i]] = 1;
+            uint32_t next_top = 0, next_rest = k;
+            for (uint32_t i = 0; i < n; i++) pos[i] = top[i] ? next_top++ : next_rest++;
+            lds_top = k;
         }
+        auto tag = [&](uint32_t l) {
+            return l >= n ? THR_END : (thr_leaf[l] ? (THR_LEAF | pos[l]) : pos[l]);
+        };
+        std::vector<DNode> placed(n);
+        for (uint32_t i = 0; i < n; i++) {
+            DNode r = thr[i];
+            r.left = tag(r.left);
+            if (!thr_leaf[i]) r.right = tag(r.right);  // a leaf's `right` is its ref
+            placed[pos[i]] = r;
+        }
+        thr_root_tagged = n == 0 ? THR_END : (thr_leaf[0] ? (THR_LEAF | pos[0]) : pos[0]);
+        thr.swap(placed);
     }
     if (thr.size() >= (1u << 26)) return fail(GS_ERR_UNSUPPORTED, "more than 2^26 top-level BVH records");
     std::vector<DSphere> sph(s->n_spheres);
@@ -1576,7 +1687,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ds->params = (KParams*)(b + o_params);
     ds->n_nodes = s->n_nodes;
     ds->thr = (const DNode*)(b + o_thr);
-    ds->thr_root = thr.empty() ? THR_END : (thr_leaf[0] ? THR_LEAF : 0u);
+    ds->thr_root = thr_root_tagged;
+    ds->lds_top = lds_top;
     ds->stack_depth = depth < 1 ? 1 : depth;
     ds->feat = (s->n_media != 0 ? GS_FEAT_MEDIA : 0) | (nested ? GS_FEAT_NESTED : 0);
     ds->fast_boxes = true;
@@ -1717,7 +1829,12 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     HIPCHK(hipMemsetAsync(ds->queue, 0, 4, st));
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+#ifdef GS_STACK_WALK
     const size_t lds = lds_bytes(ds->stack_depth);
+#else
+    const size_t lds = lds_bytes(ds->stack_depth) + (size_t)ds->lds_top * sizeof(DNode);
+    a.lds_top = ds->lds_top;
+#endif
     int per_cu = g_blocks_per_cu;
     if (per_cu <= 0) {
         int occ = 0;
