@@ -122,7 +122,8 @@ struct KParams {
     // samples [(q % cpp) * chunk, +chunk)); each item leaves its Σrgb in `partial` and
     // gs_combine_kernel sums a pixel's chunks in chunk order.  chunk == 0: one item per
     // pixel running the reference's batch loop (camera.rs:135-165) to completion.
-    uint32_t chunk, cpp, n_items, pad2;
+    uint32_t chunk, cpp, n_items;
+    uint32_t claim;  // work items a wave claims per queue atomic (its private reserve)
     double* partial;
     float* out;     // linear colour per packed pixel (nullable when out8 is set)
     uint8_t* out8;  // write_color bytes of the f64 colour per packed pixel (nullable)
@@ -706,6 +707,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 
     uint32_t st = S_NEED;
     bool qdone = false;
+    uint32_t res_base = 0, res_cnt = 0;  // the wave's reserve of claimed items (wave-uniform)
     // path state (registers)
     uint32_t sample = 0, depth = 0;
     uint64_t rng = 0;
@@ -853,16 +855,32 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         uint64_t need = __builtin_amdgcn_ballot_w64(st == S_NEED);
 #pragma unroll 1
         while (need != 0 && !qdone) {
+            // Lanes take items from the wave's reserve; an empty reserve is refilled with
+            // `claim` items by one atomic (a contended device-scope atomic per refill round
+            // cost ~5% of wave time with 8-sample items).  Items are independent, so who
+            // runs which one changes nothing in the result.
+            if (res_cnt == 0) {
+                const uint32_t leader = (uint32_t)__ffsll((long long)need) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(P->queue, P->claim);
+                base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
+                if (base >= P->n_items) {
+                    qdone = true;
+                    break;
+                }
+                res_base = base;
+                res_cnt = min(P->claim, P->n_items - base);
+            }
             const uint32_t n = (uint32_t)__popcll(need);
-            const uint32_t leader = (uint32_t)__ffsll((long long)need) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(P->queue, n);
-            base = __shfl(base, leader);
+            const uint32_t take = min(n, res_cnt);
+            const uint32_t base = res_base;
+            res_base += take;
+            res_cnt -= take;
             const uint32_t tile_px = (uint32_t)(P->tile_w * P->tile_h);
             const bool blocked8 = (P->tile_w % 8 == 0) && (P->tile_h % 8 == 0);
-            if ((uint64_t)base + n >= (uint64_t)P->n_items) qdone = true;
-            if (st == S_NEED) {
-                const uint64_t q = (uint64_t)base + (uint64_t)__popcll(need & lanemask_lt(lane));
+            const uint32_t rank = (uint32_t)__popcll(need & lanemask_lt(lane));
+            if (st == S_NEED && rank < take) {
+                const uint64_t q = (uint64_t)base + (uint64_t)rank;
                 if (q >= P->n_items) {
                     st = S_DONE;
                 } else {
@@ -1807,6 +1825,7 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     kp.chunk = chunk;
     kp.cpp = cpp;
     kp.n_items = (uint32_t)cap * cpp;
+    kp.claim = 1;  // set below, once the grid size is known
     if (chunk) {
         const size_t need = (size_t)kp.n_items * 3 * sizeof(double);
         gs_device_scene* mds = const_cast<gs_device_scene*>(ds);
@@ -1841,16 +1860,21 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     a.fast_boxes = ds->fast_boxes ? 1 : 0;
     a.shade_batch = g_shade_batch;
     a.leaf_batch = g_leaf_batch < 1 ? 1 : g_leaf_batch;  // 0 would never step a node
-    // Pageable source: the runtime stages it before returning, so `kp` may go out of scope.
-    HIPCHK(hipMemcpyAsync(ds->params, &kp, sizeof(KParams), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemsetAsync(ds->queue, 0, 4, st));
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
 #ifdef GS_STACK_WALK
     const size_t lds = lds_bytes(ds->stack_depth);
 #else
-    const size_t lds = lds_bytes(ds->stack_depth) + (size_t)ds->lds_top * sizeof(DNode);
-    a.lds_top = ds->lds_top;
+    // The mirror takes what the block's LDS limit leaves after the kernel's static LDS and
+    // the lane state (records [0, lds_top) are the best ones, so any prefix is valid).
+    hipFuncAttributes fa{};
+    HIPCHK(hipFuncGetAttributes(&fa, (const void*)kernel_for(ds->feat)));
+    int max_lds = 0;
+    HIPCHK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+    const int64_t room = (int64_t)max_lds - (int64_t)fa.sharedSizeBytes - (int64_t)lds_bytes(ds->stack_depth);
+    if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
+    a.lds_top = std::min<uint32_t>(ds->lds_top, (uint32_t)(room / (int64_t)sizeof(DNode)));
+    const size_t lds = lds_bytes(ds->stack_depth) + (size_t)a.lds_top * sizeof(DNode);
 #endif
     int per_cu = g_blocks_per_cu;
     if (per_cu <= 0) {
@@ -1863,6 +1887,15 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     int64_t max_blocks = ((int64_t)kp.n_items + GS_BLOCK - 1) / GS_BLOCK;
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks < 1) blocks = 1;
+    // Items per queue claim: about 1/64 of a wave's share of the items, at most 32 (a wave
+    // ends holding at most one partly used reserve), at least 1.
+    {
+        const uint64_t per_wave = (uint64_t)kp.n_items / ((uint64_t)blocks * (GS_BLOCK / 64));
+        kp.claim = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, per_wave / 64));
+    }
+    // Pageable source: the runtime stages it before returning, so `kp` may go out of scope.
+    HIPCHK(hipMemcpyAsync(ds->params, &kp, sizeof(KParams), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(ds->queue, 0, 4, st));
     hipLaunchKernelGGL(kernel_for(ds->feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
     if (chunk) {
