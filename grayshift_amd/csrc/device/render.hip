@@ -1232,10 +1232,10 @@ static uint32_t lds_top_budget() {
     const int64_t left = share - (int64_t)GS_BLOCK * (L_ND * 8 + L_NI * 4) - 1024;  // 1 KiB: static LDS + slack
     return left > 0 ? (uint32_t)(left / 64) : 0u;
 }
-// -1 auto, 0 never split a pixel's samples.  Swept on MI355X, C4 rank 0 of N
-// (tools/rank_sim.py; ms): N=1: 32 -> 808.7, 16 -> 803.2, 8 -> 804.9, 4 -> 805.2;
-// N=8: 32 -> 113.3, 16 -> 110.2, 8 -> 107.4, 4 -> 107.5.  Small chunks cost nothing at
-// one GPU and shorten the queue's tail when a rank holds few pixels per lane.
+// -1 auto, 0 never split a pixel's samples.  Swept on MI355X with batched queue claims,
+// C4 rank 0 / rank 3 of N (tools/rank_sim.py; ms): N=1: 4 -> 658.4, 8 -> 658.7,
+// 16 -> 648.3, 32 -> 647.3; N=8: 4 -> 89.6, 8 -> 89.6, 16 -> 89.7, 32 -> 95.8 (max of the
+// two ranks).  16 is within noise of the best at both ends.
 static int32_t g_sample_chunk = -1;
 static const uint64_t kPartialBudget = 4ull << 30;  // auto chunks: at most 4 GiB of chunk sums
 
@@ -1812,7 +1812,7 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     uint32_t chunk = 0, cpp = 1;
     if (g_sample_chunk != 0 && ss->max_samples < ss->batch_size) {
         const uint32_t bs = ss->batch_size;
-        uint32_t c = g_sample_chunk > 0 ? (uint32_t)g_sample_chunk : std::max<uint32_t>(8u, (bs + 63u) / 64u);
+        uint32_t c = g_sample_chunk > 0 ? (uint32_t)g_sample_chunk : std::max<uint32_t>(16u, (bs + 63u) / 64u);
         if ((bs + c - 1) / c > 64u) c = (bs + 63u) / 64u;  // at most 64 chunks per pixel
         if (g_sample_chunk < 0)
             while (c < bs && (uint64_t)cap * ((bs + c - 1) / c) * 24u > kPartialBudget) c *= 2u;

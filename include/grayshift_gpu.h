@@ -208,7 +208,7 @@ int32_t gs_version(void);
  * occupancy query; leaf_batch in [0, 64] = lanes waiting at a leaf before the wave
  * runs a leaf-test pass (0 acts as 1);
  * sample_chunk = samples per work item when the settings run a single batch
- * (max_samples < batch_size, as every fixed-spp render): -1 auto (8, or batch/64 for
+ * (max_samples < batch_size, as every fixed-spp render): -1 auto (16, or batch/64 for
  * big batches: at most 64 chunks per pixel, and at most 4 GiB of chunk sums), 0 never
  * split a pixel, n > 0 explicit.
  * Chunks keep every sample's RNG stream; a pixel's chunk sums are added in sample order,
