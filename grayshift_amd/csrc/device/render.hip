@@ -525,13 +525,16 @@ __device__ GS_NOINLINE d3 background(const DevScene& sc, d3 dir, unsigned long l
     d3 rv = mk(dir.x * bg.rot[0] + dir.y * bg.rot[1] + dir.z * bg.rot[2],
                dir.x * bg.rot[3] + dir.y * bg.rot[4] + dir.z * bg.rot[5],
                dir.x * bg.rot[6] + dir.y * bg.rot[7] + dir.z * bg.rot[8]);
-    d3 rot = unit(rv);
-    double theta = atan2(rot.y, rot.x);
-    double phi = asin(rot.z);
-    double u = 0.5 + theta / (2.0 * PI);
-    double v = 0.5 - phi / PI;
-    uint64_t x = sat_u64(u * (double)bg.width, 18446744073709551616.0, ~0ull) % (uint64_t)bg.width;
-    uint64_t y = sat_u64(v * (double)bg.height, 18446744073709551616.0, ~0ull) % (uint64_t)bg.height;
+    uint64_t x, y;
+    {
+        d3 rot = unit(rv);
+        double theta = atan2(rot.y, rot.x);
+        double phi = asin(rot.z);
+        double u = 0.5 + theta / (2.0 * PI);
+        double v = 0.5 - phi / PI;
+        x = sat_u64(u * (double)bg.width, 18446744073709551616.0, ~0ull) % (uint64_t)bg.width;
+        y = sat_u64(v * (double)bg.height, 18446744073709551616.0, ~0ull) % (uint64_t)bg.height;
+    }
     const uint64_t k = y * (uint64_t)bg.width + x;
     atomicAdd(&cnt[C_HDRI], 1ull);
     if (sc.hdri_rgbe) {
@@ -742,9 +745,11 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         LD(L_CSR) += Lr;
         LD(L_CSG) += Lg;
         LD(L_CSB) += Lb;
-        double lum = 0.299 * Lr + 0.587 * Lg + 0.144 * Lb;
-        LD(L_LSUM) += lum;
-        LD(L_LSQ) += lum * lum;
+        if (!P->chunk) {  // a chunk never reaches the stop test: Σlum, Σlum² unused
+            double lum = 0.299 * Lr + 0.587 * Lg + 0.144 * Lb;
+            LD(L_LSUM) += lum;
+            LD(L_LSQ) += lum * lum;
+        }
         sample++;
         LI(L_BLEFT) -= 1u;
     };
