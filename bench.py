@@ -115,14 +115,18 @@ def main():
         if timed:
             kernel_ms.append((ev0, ev1))
 
+    # The counter accumulation runs in the warm-up too: the first torch int64 add loads its
+    # kernel (~13 ms), which must not land in the timed region.
+    tot = torch.zeros(16, dtype=torch.int64, device=dev)
     for _ in range(a.warmup):
         step(False)
+        tot += counters
     torch.cuda.synchronize()
+    tot.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    tot = torch.zeros(16, dtype=torch.int64, device=dev)
     for _ in range(a.steps):
         step(True)
         tot += counters

@@ -1173,6 +1173,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     if (threadIdx.x < C_N && P->counters) atomicAdd(&P->counters[threadIdx.x], s_cnt[threadIdx.x]);
 }
 
+// Per-launch parameters reach device memory by a one-thread kernel on the caller's stream
+// (not a pageable hipMemcpyAsync, which can block the host until earlier work drains and
+// would need a host buffer that outlives the copy).
+__global__ void gs_params_kernel(KParams kp, KParams* __restrict__ dst) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *dst = kp;
+}
+
 // Chunked single-batch renders: a pixel's colour is the sum of its chunks' Σrgb, taken
 // in chunk (= sample) order, over the batch size (camera.rs:142-160 with one batch).
 // Padding slots of partial tiles get zeros.
@@ -1269,6 +1276,11 @@ struct gs_device_scene {
     const DNode* thr = nullptr;  // threaded top-level records (THR_END)
     uint32_t thr_root = THR_END;
     uint32_t lds_top = 0;        // records mirrored in LDS per block
+    // launch geometry, computed at the first launch (host API queries cost ~0.5 ms each)
+    bool launch_ready = false;
+    int cus = 0, per_cu = 0;
+    uint32_t launch_lds_top = 0;
+    size_t launch_lds = 0;
     double* partial = nullptr;  // chunk partial sums, grown on demand
     size_t partial_bytes = 0;
 };
@@ -1865,28 +1877,33 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     a.fast_boxes = ds->fast_boxes ? 1 : 0;
     a.shade_batch = g_shade_batch;
     a.leaf_batch = g_leaf_batch < 1 ? 1 : g_leaf_batch;  // 0 would never step a node
-    int cus = 0;
-    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    gs_device_scene* mds = const_cast<gs_device_scene*>(ds);
+    if (!mds->launch_ready) {
+        HIPCHK(hipDeviceGetAttribute(&mds->cus, hipDeviceAttributeMultiprocessorCount, dev));
 #ifdef GS_STACK_WALK
-    const size_t lds = lds_bytes(ds->stack_depth);
+        mds->launch_lds_top = 0;
+        mds->launch_lds = lds_bytes(ds->stack_depth);
 #else
-    // The mirror takes what the block's LDS limit leaves after the kernel's static LDS and
-    // the lane state (records [0, lds_top) are the best ones, so any prefix is valid).
-    hipFuncAttributes fa{};
-    HIPCHK(hipFuncGetAttributes(&fa, (const void*)kernel_for(ds->feat)));
-    int max_lds = 0;
-    HIPCHK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
-    const int64_t room = (int64_t)max_lds - (int64_t)fa.sharedSizeBytes - (int64_t)lds_bytes(ds->stack_depth);
-    if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
-    a.lds_top = std::min<uint32_t>(ds->lds_top, (uint32_t)(room / (int64_t)sizeof(DNode)));
-    const size_t lds = lds_bytes(ds->stack_depth) + (size_t)a.lds_top * sizeof(DNode);
+        // The mirror takes what the block's LDS limit leaves after the kernel's static LDS
+        // and the lane state (records [0, lds_top) are the best ones, so any prefix is valid).
+        hipFuncAttributes fa{};
+        HIPCHK(hipFuncGetAttributes(&fa, (const void*)kernel_for(ds->feat)));
+        int max_lds = 0;
+        HIPCHK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+        const int64_t room = (int64_t)max_lds - (int64_t)fa.sharedSizeBytes - (int64_t)lds_bytes(ds->stack_depth);
+        if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
+        mds->launch_lds_top = std::min<uint32_t>(ds->lds_top, (uint32_t)(room / (int64_t)sizeof(DNode)));
+        mds->launch_lds = lds_bytes(ds->stack_depth) + (size_t)mds->launch_lds_top * sizeof(DNode);
 #endif
-    int per_cu = g_blocks_per_cu;
-    if (per_cu <= 0) {
         int occ = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel_for(ds->feat), GS_BLOCK, lds));
-        per_cu = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel_for(ds->feat), GS_BLOCK, mds->launch_lds));
+        mds->per_cu = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
+        mds->launch_ready = true;
     }
+    const int cus = ds->cus;
+    const size_t lds = ds->launch_lds;
+    a.lds_top = ds->launch_lds_top;
+    const int per_cu = g_blocks_per_cu > 0 ? g_blocks_per_cu : ds->per_cu;
     int64_t blocks = (int64_t)cus * per_cu;
     // no more waves than work: one lane per item at most
     int64_t max_blocks = ((int64_t)kp.n_items + GS_BLOCK - 1) / GS_BLOCK;
@@ -1898,8 +1915,8 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
         const uint64_t per_wave = (uint64_t)kp.n_items / ((uint64_t)blocks * (GS_BLOCK / 64));
         kp.claim = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, per_wave / 64));
     }
-    // Pageable source: the runtime stages it before returning, so `kp` may go out of scope.
-    HIPCHK(hipMemcpyAsync(ds->params, &kp, sizeof(KParams), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(gs_params_kernel, dim3(1), dim3(64), 0, st, kp, ds->params);
+    HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(ds->queue, 0, 4, st));
     hipLaunchKernelGGL(kernel_for(ds->feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
