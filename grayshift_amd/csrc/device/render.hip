@@ -1075,6 +1075,30 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                 }
                 cur = next;
+#ifndef GS_LEAF_RUN
+#define GS_LEAF_RUN 2
+#endif
+                // More leaves in the same pass while the next record is a leaf holding a
+                // stationary sphere (the n == 2 leaves of BVH.rs:44-55 sit side by side):
+                // up to GS_LEAF_RUN per pass, each tested in order with the updated closest.
+#pragma unroll 1
+                for (int k = 1; k < GS_LEAF_RUN && cur > THR_END; k++) {
+                    const uint32_t l2 = cur & ~THR_LEAF;
+                    if (l2 < A.lds_top) {
+                        load_leaf_rec_lds(s_top + (l2 << 6), scx, scy, scz, sr, next, ref);
+                    } else {
+                        load_leaf_rec((const DNode*)((const char*)A.nodes + (l2 << 6)), scx, scy, scz, sr, next, ref);
+                    }
+                    if ((ref >> GS_REF_SHIFT) != GS_REF_SPHERE) break;
+                    c_sph++;
+                    double t;
+                    if (sphere_accept(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
+                        closest = t;
+                        hit_ref = ref;
+                        hit_inst = GS_REF_NONE;
+                    }
+                    cur = next;
+                }
             }
             st = (tracing && cur == THR_END) ? (uint32_t)S_SHADE : st;
 #endif

@@ -89,12 +89,12 @@ class HostScene:
 class Renderer:
     """A scene resident in HBM of the current device, rendered tile-partitioned."""
 
-    def __init__(self, scene, rank=0, world_size=1, tile=64):
+    def __init__(self, scene, rank=0, world_size=1, tile=64, tile_h=None):
         self.scene = scene
         self.host = HostScene(scene.spec)
         self.cam = camera(scene.camera)
         self.settings = scene.settings
-        self.part = N.gs_partition(rank=rank, world_size=world_size, tile_w=tile, tile_h=tile)
+        self.part = N.gs_partition(rank=rank, world_size=world_size, tile_w=tile, tile_h=tile_h or tile)
         self.capacity = N.lib.gs_partition_capacity(C.byref(self.cam), C.byref(self.part))
         if self.capacity < 0:
             raise ValueError("bad partition")

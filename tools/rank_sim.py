@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--config", default="C4")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--tiles", default="64")
+    ap.add_argument("--tile-h", type=int, default=0, help="tile height (default: square tiles)")
     a = ap.parse_args()
     import torch
     import grayshift_amd as g
@@ -38,7 +39,7 @@ def main():
             for rank in [int(x) for x in a.ranks.split(",")]:
                 if rank >= world:
                     continue
-                r = g.Renderer(sc, rank=rank, world_size=world, tile=tile)
+                r = g.Renderer(sc, rank=rank, world_size=world, tile=tile, tile_h=a.tile_h or tile)
                 out = torch.zeros(r.capacity * 3, dtype=torch.float32, device=dev)
                 cnt = torch.zeros(16, dtype=torch.int64, device=dev)
                 r.render_async(out.data_ptr(), cnt.data_ptr(), stream.cuda_stream, seed=1)  # warm-up
