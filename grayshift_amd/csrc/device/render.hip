@@ -44,7 +44,6 @@ using namespace gsd;
 #ifndef GS_BLOCK
 #define GS_BLOCK 1024
 #endif
-#define GS_STACK 32  // max BVH depth the device accepts
 // Measured on MI355X (C4): everything inlined with a 4-waves/SIMD register cap (128
 // VGPRs; spills only in shading) beats out-of-line shading calls and 3 or 5 waves.
 #ifndef GS_NOINLINE
@@ -158,7 +157,7 @@ __host__ __device__ inline uint32_t device_ref(uint32_t abi_ref) {
     return abi_ref;
 }
 
-// Threaded top-level tree (the default walk; -DGS_STACK_WALK keeps the LDS-stack walk).
+// Threaded top-level tree.
 // BVHNode::hit's left-first recursion (BVH.rs:69-90) visits the tree in pre-order, and a
 // box miss skips exactly the node's subtree.  So the top-level tree is stored as its
 // pre-order sequence of records — one per node AND one per leaf occurrence — where a node
@@ -662,17 +661,11 @@ __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull <<
 #endif
 
 // Per-lane pixel state lives in LDS ([field][lane], conflict-free), touched once per
-// path; the traversal stack follows it: [depth][lane] u32 refs.
+// path; the mirror of the tree's top records follows it.
 enum { L_CSR = 0, L_CSG, L_CSB, L_LSUM, L_LSQ, L_SCOUNT, L_ND };
 enum { L_ITEM = 0, L_PIX, L_BLEFT, L_NI };
 
-__host__ __device__ inline size_t lds_bytes(uint32_t stack_depth) {
-#ifdef GS_STACK_WALK
-    return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4 + (stack_depth + 1) * 4);  // + the dummy slot 0
-#else
-    return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4);  // the threaded walk keeps no stack
-#endif
-}
+__host__ __device__ constexpr size_t lane_lds_bytes() { return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4); }
 
 template <int FEAT>
 __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs A) {
@@ -684,18 +677,15 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #endif
     double* s_d = (double*)smem;                                  // [L_ND][GS_BLOCK]
     uint32_t* s_i = (uint32_t*)(smem + L_ND * 8 * GS_BLOCK);      // [L_NI][GS_BLOCK]
-    uint32_t* s_stack = s_i + L_NI * GS_BLOCK;                    // [depth][GS_BLOCK]
-#ifndef GS_STACK_WALK
-    // The hottest threaded records (the tree's top levels, placed first by the host) are
-    // mirrored in LDS: a node step then reads them through a flat pointer that resolves to
-    // LDS for those records and to global memory for the rest, per lane.
-    uint8_t* s_top = smem + lds_bytes(0);
+    // The records a ray most likely tests (placed first by the host) are mirrored in LDS;
+    // a lane whose record index is below lds_top reads it from there (ds_read), the rest
+    // from global memory.
+    uint8_t* s_top = smem + lane_lds_bytes();
     {
         const uint4* src = reinterpret_cast<const uint4*>(A.nodes);
         uint4* dst = reinterpret_cast<uint4*>(s_top);
         for (uint32_t k = threadIdx.x; k < A.lds_top * 4u; k += GS_BLOCK) dst[k] = src[k];
     }
-#endif
     if (threadIdx.x < C_N) s_cnt[threadIdx.x] = 0;
     __syncthreads();
 
@@ -721,7 +711,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     ray.time = 0;
     d3 inv = mk(0, 0, 0);
     // traversal state
-    uint32_t cur = DREF_NONE, sp = 0, hit_ref = GS_REF_NONE, hit_inst = GS_REF_NONE;
+    uint32_t cur = THR_END, hit_ref = GS_REF_NONE, hit_inst = GS_REF_NONE;
     double closest = 0.0;
     bool fast = false;  // this ray's slab times can never be NaN (geometry.hpp box_hit_fast)
     // hot counters kept in registers, flushed per pixel
@@ -732,8 +722,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #ifndef GS_NO_FAST_SLAB
         fast = A.fast_boxes && fast_slab_ray(ray.o, inv);
 #endif
-        cur = A.root;  // a device ref (DREF_*)
-        sp = 0;
+        cur = A.root;  // the root record's link (THR_*)
         closest = 1.7976931348623157e308;  // f64::MAX (camera.rs:177)
         hit_ref = GS_REF_NONE;
         hit_inst = GS_REF_NONE;
@@ -967,13 +956,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             // do), then test those leaves together, so a wave pays for the node step and the
             // sphere test in different iterations instead of both in every one.  Each lane
             // still processes its refs in the reference's order.  The pass kind is uniform.
-#ifdef GS_STACK_WALK
-            const bool at_leaf = tracing && cur >= DREF_LEAF;
-            const uint64_t lm = tr & __builtin_amdgcn_ballot_w64(cur >= DREF_LEAF);  // == ballot(at_leaf)
-#else
             const bool at_leaf = tracing && cur > THR_END;
             const uint64_t lm = tr & __builtin_amdgcn_ballot_w64(cur > THR_END);  // == ballot(at_leaf)
-#endif
             const bool leaf_pass = lm == tr || (uint32_t)__popcll(lm) >= (uint32_t)A.leaf_batch;
 #ifdef GS_STAMPS
             it_all++;
@@ -982,54 +966,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             ln_node += leaf_pass ? 0ull : (uint64_t)__popcll(tr & ~lm);
             ln_leaf += leaf_pass ? (uint64_t)__popcll(lm) : 0ull;
 #endif
-#ifdef GS_STACK_WALK
-            if (!leaf_pass) {
-                if (tracing && !at_leaf) {
-                    // All 64 B in one go (4 x dwordx4) and a branchless push: the child refs
-                    // are always consumed, so the compiler cannot defer their load behind
-                    // the box test (a second dependent memory round trip).  Device node refs
-                    // are bare indices: byte offset = cur << 6, one VALU op off the SGPR base.
-                    const DNode nd = load_node((const DNode*)((const char*)A.nodes + (cur << 6)));
-                    c_nodes++;
-                    bool h;
-                    if (wave_fast) {
-                        h = box_hit_fast(nd, ray.o, inv, tmin, closest);
-                    } else {
-                        h = box_hit(nd, ray.o, inv, tmin, closest);
-                    }
-                    s_stack[(sp + 1u) * GS_BLOCK + tid] = nd.right;  // slot sp+1 <= BVH depth
-                    sp += (h && nd.right != DREF_NONE) ? 1u : 0u;
-                    cur = h ? nd.left : DREF_NONE;
-                }
-            } else if (at_leaf) {
-                if ((cur >> GS_REF_SHIFT) == GS_REF_SPHERE) {
-                    c_sph++;
-                    const DSphere s = *(const DSphere*)((const char*)A.spheres + (cur << 5));
-                    double t;
-                    if (sphere_accept(mk(s.cx, s.cy, s.cz), s.r, ray, len2(ray.d), tmin, closest, t)) {
-                        closest = t;
-                        hit_ref = cur;
-                        hit_inst = GS_REF_NONE;
-                    }
-                } else {
-                    const LeafHit lh = leaf_other<FEAT>(sc, cur, ray, tmin, closest, rng, s_cnt);
-                    if (lh.hit) {
-                        closest = lh.t;
-                        hit_ref = lh.ref;
-                        hit_inst = lh.inst;
-                    }
-                }
-                cur = DREF_NONE;
-            }
-            // Branchless pop.  Entry k of the stack lives in slot k + 1 and slot 0 is a
-            // dummy, so the read below is in bounds for every sp in [0, depth].
-            const bool empty = tracing && cur == DREF_NONE;
-            const bool pop = empty && sp != 0;
-            const uint32_t top = s_stack[sp * GS_BLOCK + tid];
-            cur = pop ? top : cur;
-            sp -= pop ? 1u : 0u;
-            st = (empty && !pop) ? (uint32_t)S_SHADE : st;
-#else
             if (!leaf_pass) {
                 if (tracing && !at_leaf) {
                     // One 64-B record (4 x dwordx4 off the SGPR base, offset = cur << 6), the
@@ -1101,7 +1037,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 }
             }
             st = (tracing && cur == THR_END) ? (uint32_t)S_SHADE : st;
-#endif
         }
 
         // ---------------------------------------------------------- shade
@@ -1294,7 +1229,7 @@ struct gs_device_scene {
     KParams* params = nullptr;  // per-launch cold parameters (device memory)
     DevScene dev{};
     uint32_t n_nodes = 0;
-    uint32_t stack_depth = 1;  // LDS stack entries per lane (= BVH depth)
+    uint32_t bvh_depth = 1;  // top-level BVH depth (informational: the walk keeps no stack)
     bool fast_boxes = false;  // every node coordinate |x| < 1e300
     int feat = 0;             // GS_FEAT_* of the kernel instantiation to launch
     const DNode* thr = nullptr;  // threaded top-level records (THR_END)
@@ -1438,7 +1373,6 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
                                      "that is not a primitive");
         }
     }
-    if (maxd > GS_STACK) return unsup("BVH deeper than the device stack (" + std::to_string(GS_STACK) + ")");
     *depth_out = maxd;
     *nested_out = nested;
     auto mat_ok = [&](uint32_t m) { return m < s.n_materials; };
@@ -1765,7 +1699,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ds->thr = (const DNode*)(b + o_thr);
     ds->thr_root = thr_root_tagged;
     ds->lds_top = lds_top;
-    ds->stack_depth = depth < 1 ? 1 : depth;
+    ds->bvh_depth = depth < 1 ? 1 : depth;
     ds->feat = (s->n_media != 0 ? GS_FEAT_MEDIA : 0) | (nested ? GS_FEAT_NESTED : 0);
     ds->fast_boxes = true;
     for (uint32_t i = 0; i < s->n_nodes && ds->fast_boxes; i++)
@@ -1886,39 +1820,26 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     kp.queue = ds->queue;
     kp.item_visits = outs->item_visits;
     KArgs a{};
-#ifdef GS_STACK_WALK
-    a.nodes = ds->dev.nodes;
-#else
     a.nodes = ds->thr;
-#endif
     a.spheres = ds->dev.spheres;
     a.P = ds->params;
-#ifdef GS_STACK_WALK
-    a.root = ds->dev.root;
-#else
     a.root = ds->thr_root;
-#endif
     a.fast_boxes = ds->fast_boxes ? 1 : 0;
     a.shade_batch = g_shade_batch;
     a.leaf_batch = g_leaf_batch < 1 ? 1 : g_leaf_batch;  // 0 would never step a node
     gs_device_scene* mds = const_cast<gs_device_scene*>(ds);
     if (!mds->launch_ready) {
         HIPCHK(hipDeviceGetAttribute(&mds->cus, hipDeviceAttributeMultiprocessorCount, dev));
-#ifdef GS_STACK_WALK
-        mds->launch_lds_top = 0;
-        mds->launch_lds = lds_bytes(ds->stack_depth);
-#else
         // The mirror takes what the block's LDS limit leaves after the kernel's static LDS
         // and the lane state (records [0, lds_top) are the best ones, so any prefix is valid).
         hipFuncAttributes fa{};
         HIPCHK(hipFuncGetAttributes(&fa, (const void*)kernel_for(ds->feat)));
         int max_lds = 0;
         HIPCHK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
-        const int64_t room = (int64_t)max_lds - (int64_t)fa.sharedSizeBytes - (int64_t)lds_bytes(ds->stack_depth);
+        const int64_t room = (int64_t)max_lds - (int64_t)fa.sharedSizeBytes - (int64_t)lane_lds_bytes();
         if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
         mds->launch_lds_top = std::min<uint32_t>(ds->lds_top, (uint32_t)(room / (int64_t)sizeof(DNode)));
-        mds->launch_lds = lds_bytes(ds->stack_depth) + (size_t)mds->launch_lds_top * sizeof(DNode);
-#endif
+        mds->launch_lds = lane_lds_bytes() + (size_t)mds->launch_lds_top * sizeof(DNode);
         int occ = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel_for(ds->feat), GS_BLOCK, mds->launch_lds));
         mds->per_cu = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
