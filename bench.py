@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--width", type=int, default=None, help="override (testing only; invalidates the metric)")
     ap.add_argument("--spp", type=int, default=None, help="override (testing only; invalidates the metric)")
     ap.add_argument("--tile", type=int, default=64)
+    ap.add_argument("--no-plan", action="store_true",
+                    help="N>1: round-robin tiles instead of the cost-balanced plan (gs_plan_tiles)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--shade-batch", type=int, default=None)
     ap.add_argument("--blocks-per-cu", type=int, default=None)
@@ -82,11 +84,13 @@ def main():
     g.set_tuning(a.shade_batch or 52, a.blocks_per_cu or 0, 8 if a.leaf_batch is None else a.leaf_batch,
                  -1 if a.sample_chunk is None else a.sample_chunk)
     sc = scenes.config(a.config, width=a.width, spp=a.spp)
-    r = g.Renderer(sc, rank=rank, world_size=world, tile=a.tile)
-    # Every rank's packed buffer has rank 0's capacity (round-robin gives it the most tiles)
-    cap0 = g._native.lib.gs_partition_capacity(
-        __import__("ctypes").byref(r.cam),
-        __import__("ctypes").byref(g._native.gs_partition(0, world, a.tile, a.tile)))
+    # N > 1: tiles are assigned by a cost-balanced plan computed once at setup (a 1-spp pilot
+    # of the frame, identical on every rank; outside the timed region, like the BVH build).
+    plan = world > 1 and not a.no_plan
+    r = g.Renderer(sc, rank=rank, world_size=world, tile=a.tile, plan=plan)
+    # Every rank's packed buffer has rank 0's capacity (the most tiles any rank holds)
+    p0 = g._native.gs_partition(0, world, a.tile, a.tile, r.part.d_tile_order, r.part.slots_per_rank, 0)
+    cap0 = g._native.lib.gs_partition_capacity(__import__("ctypes").byref(r.cam), __import__("ctypes").byref(p0))
     dev = torch.device("cuda", local)
     packed = torch.zeros(cap0 * 3, dtype=torch.float32, device=dev)
     counters = torch.zeros(16, dtype=torch.int64, device=dev)
@@ -187,7 +191,8 @@ def main():
                 "workload": "%s: %s %dx%d, %d spp%s" % (a.config, sc.name, r.width, r.height,
                                                       sc.settings.batch_size,
                                                       " (OVERRIDDEN: not the metric)" if invalid else ""),
-                "tile": a.tile, "parallelism": "tiles%d" % world, "seed": a.seed,
+                "tile": a.tile, "parallelism": "tiles%d" % world, "tile_plan": "cost-balanced" if plan else "round-robin",
+                "seed": a.seed,
                 "rays_per_frame": rays_per_frame, "paths_per_frame": c["paths"],
                 "node_visits_per_ray": round(c["node_visits"] / max(1, rays_per_frame), 3),
             },

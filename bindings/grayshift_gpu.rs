@@ -90,8 +90,11 @@ pub struct gs_camera {
 #[repr(C)] #[derive(Clone, Copy, Default)]
 pub struct gs_sample_settings { pub confidence: f64, pub tolerance: f64, pub batch_size: u32, pub max_samples: u32 }
 
-#[repr(C)] #[derive(Clone, Copy, Default)]
-pub struct gs_partition { pub rank: i32, pub world_size: i32, pub tile_w: i32, pub tile_h: i32 }
+#[repr(C)] #[derive(Clone, Copy)]
+pub struct gs_partition {
+    pub rank: i32, pub world_size: i32, pub tile_w: i32, pub tile_h: i32,
+    pub d_tile_order: *const i32, pub slots_per_rank: i32, pub pad: i32,
+}
 
 #[repr(C)] #[derive(Clone, Copy, Default)]
 pub struct gs_counters {
@@ -131,6 +134,15 @@ extern "C" {
                                     stream: *mut c_void) -> gs_status;
     pub fn gs_unpack_tiles_u8_async(cam: *const gs_camera, world_size: i32, tile_w: i32, tile_h: i32, capacity: i64,
                                     d_gathered: *const u8, d_frame: *mut u8, stream: *mut c_void) -> gs_status;
+    pub fn gs_plan_tiles(scene: *const gs_device_scene, cam: *const gs_camera, seed: u64, world_size: i32,
+                         tile_w: i32, tile_h: i32, order_out: *mut i32, order_cap: i64,
+                         slots_per_rank: *mut i32) -> gs_status;
+    pub fn gs_unpack_tiles_part_async(cam: *const gs_camera, part: *const gs_partition, capacity: i64,
+                                      d_gathered: *const c_void, d_frame: *mut c_void, elem_bytes: i32,
+                                      stream: *mut c_void) -> gs_status;
+    pub fn gs_device_alloc(bytes: i64, d_out: *mut *mut c_void) -> gs_status;
+    pub fn gs_device_free(d_ptr: *mut c_void) -> gs_status;
+    pub fn gs_device_upload(d_dst: *mut c_void, host_src: *const c_void, bytes: i64) -> gs_status;
     pub fn gs_ppm_max_bytes(width: i32, height: i32) -> i64;
     pub fn gs_ppm_scratch_bytes(width: i32, height: i32) -> i64;
     pub fn gs_ppm_encode_async(d_rgb8: *const u8, width: i32, height: i32, d_text: *mut c_char, text_capacity: i64,

@@ -90,7 +90,8 @@ class gs_medium_rec(C.Structure):  # gs_medium (a flat-scene record)
 
 
 class gs_partition(C.Structure):
-    _fields_ = [("rank", C.c_int32), ("world_size", C.c_int32), ("tile_w", C.c_int32), ("tile_h", C.c_int32)]
+    _fields_ = [("rank", C.c_int32), ("world_size", C.c_int32), ("tile_w", C.c_int32), ("tile_h", C.c_int32),
+                ("d_tile_order", C.c_void_p), ("slots_per_rank", C.c_int32), ("pad", C.c_int32)]
 
 
 class gs_background(C.Structure):
@@ -147,6 +148,13 @@ SIGNATURES = {
     "gs_ppm_encode_async": (C.c_int32, [_P, C.c_int32, C.c_int32, _P, C.c_int64, _P, _P, C.c_int64, _P]),
     "gs_render_ppm": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64, _P,
                                   C.c_int64, C.POINTER(C.c_int64), C.POINTER(gs_counters)]),
+    "gs_plan_tiles": (C.c_int32, [_P, C.POINTER(gs_camera), C.c_uint64, C.c_int32, C.c_int32, C.c_int32, _P,
+                                  C.c_int64, C.POINTER(C.c_int32)]),
+    "gs_unpack_tiles_part_async": (C.c_int32, [C.POINTER(gs_camera), C.POINTER(gs_partition), C.c_int64, _P, _P,
+                                               C.c_int32, _P]),
+    "gs_device_alloc": (C.c_int32, [C.c_int64, C.POINTER(_P)]),
+    "gs_device_free": (C.c_int32, [_P]),
+    "gs_device_upload": (C.c_int32, [_P, _P, C.c_int64]),
     "gs_render": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64, _P,
                               C.POINTER(gs_counters)]),
     # grayshift_host.h

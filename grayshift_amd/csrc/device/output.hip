@@ -202,7 +202,7 @@ struct VecOf<1> { using T = uint8_t; };
 template <int V>
 __global__ void gs_unpack_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ frame, uint32_t E, int32_t W,
                                  int32_t H, int32_t world, int32_t tile_w, int32_t tile_h, int32_t tiles_x,
-                                 uint64_t capacity) {
+                                 uint64_t capacity, const int32_t* __restrict__ order) {
     using T = typename VecOf<V>::T;
     const uint64_t run = (uint64_t)tile_w * E;  // bytes per tile row
     const uint64_t rank_bytes = capacity * E;
@@ -215,7 +215,9 @@ __global__ void gs_unpack_kernel(const uint8_t* __restrict__ in, uint8_t* __rest
         const uint64_t row = rb / run;  // slot * tile_h + ty
         const uint64_t o = rb - row * run;
         const uint32_t slot = (uint32_t)(row / (uint64_t)tile_h), ty = (uint32_t)(row % (uint64_t)tile_h);
-        const uint32_t tile = r + slot * (uint32_t)world;
+        const uint32_t pos = r + slot * (uint32_t)world;
+        const uint32_t tile = order ? (uint32_t)order[pos] : pos;
+        if (tile == 0xFFFFFFFFu) continue;  // an empty slot of a planned partition
         const uint64_t x0b = (uint64_t)(tile % (uint32_t)tiles_x) * (uint64_t)tile_w * E;
         const uint32_t y = (tile / (uint32_t)tiles_x) * (uint32_t)tile_h + ty;
         if (y < (uint32_t)H && x0b + o < row_bytes)
@@ -224,7 +226,7 @@ __global__ void gs_unpack_kernel(const uint8_t* __restrict__ in, uint8_t* __rest
 }
 
 gs_status unpack(const gs_camera* cam, int32_t world_size, int32_t tile_w, int32_t tile_h, int64_t capacity,
-                 const void* d_in, void* d_frame, uint32_t E, void* stream);
+                 const void* d_in, void* d_frame, uint32_t E, void* stream, const int32_t* order = nullptr);
 
 gs_status fail(gs_status code, const std::string& msg) {
     gs_set_last_error(msg.c_str());
@@ -245,7 +247,7 @@ uint32_t ppm_blocks(int32_t W, int32_t H) {
 }
 
 gs_status unpack(const gs_camera* cam, int32_t world_size, int32_t tile_w, int32_t tile_h, int64_t capacity,
-                 const void* d_in, void* d_frame, uint32_t E, void* stream) {
+                 const void* d_in, void* d_frame, uint32_t E, void* stream, const int32_t* order) {
     if (!cam || !d_in || !d_frame || capacity < 0 || world_size < 1 || tile_w < 1 || tile_h < 1 ||
         cam->image_width < 1 || cam->image_height < 1)
         return fail(GS_ERR_ARG, "bad argument");
@@ -265,13 +267,13 @@ gs_status unpack(const gs_camera* cam, int32_t world_size, int32_t tile_w, int32
     uint8_t* fr = (uint8_t*)d_frame;
     if (vec == 16)
         hipLaunchKernelGGL(gs_unpack_kernel<16>, dim3(grid), dim3(256), 0, st, in, fr, E, W, H, world_size, tile_w,
-                           tile_h, tiles_x, (uint64_t)capacity);
+                           tile_h, tiles_x, (uint64_t)capacity, order);
     else if (vec == 4)
         hipLaunchKernelGGL(gs_unpack_kernel<4>, dim3(grid), dim3(256), 0, st, in, fr, E, W, H, world_size, tile_w,
-                           tile_h, tiles_x, (uint64_t)capacity);
+                           tile_h, tiles_x, (uint64_t)capacity, order);
     else
         hipLaunchKernelGGL(gs_unpack_kernel<1>, dim3(grid), dim3(256), 0, st, in, fr, E, W, H, world_size, tile_w,
-                           tile_h, tiles_x, (uint64_t)capacity);
+                           tile_h, tiles_x, (uint64_t)capacity, order);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(GS_ERR_HIP, hipGetErrorString(e));
     return GS_OK;
@@ -318,6 +320,16 @@ gs_status gs_ppm_encode_async(const uint8_t* d_rgb8, int32_t width, int32_t heig
 gs_status gs_unpack_tiles_u8_async(const gs_camera* cam, int32_t world_size, int32_t tile_w, int32_t tile_h,
                                    int64_t capacity, const uint8_t* d_in, uint8_t* d_frame, void* stream) {
     return unpack(cam, world_size, tile_w, tile_h, capacity, d_in, d_frame, 3, stream);
+}
+
+gs_status gs_unpack_tiles_part_async(const gs_camera* cam, const gs_partition* part, int64_t capacity,
+                                     const void* d_in, void* d_frame, int32_t elem_bytes, void* stream) {
+    if (!part || (elem_bytes != 12 && elem_bytes != 3)) return fail(GS_ERR_ARG, "bad argument");
+    if (part->d_tile_order && (part->slots_per_rank <= 0 ||
+                               capacity != (int64_t)part->slots_per_rank * part->tile_w * part->tile_h))
+        return fail(GS_ERR_ARG, "capacity does not match the planned partition");
+    return unpack(cam, part->world_size, part->tile_w, part->tile_h, capacity, d_in, d_frame, (uint32_t)elem_bytes,
+                  stream, part->d_tile_order);
 }
 
 gs_status gs_unpack_tiles_async(const gs_camera* cam, int32_t world_size, int32_t tile_w, int32_t tile_h,

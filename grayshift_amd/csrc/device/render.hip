@@ -123,6 +123,7 @@ struct KParams {
     // pixel running the reference's batch loop (camera.rs:135-165) to completion.
     uint32_t chunk, cpp, n_items;
     uint32_t claim;  // work items a wave claims per queue atomic (its private reserve)
+    const int32_t* order;  // position -> tile (gs_partition.d_tile_order), or null: tile = position
     double* partial;
     float* out;     // linear colour per packed pixel (nullable when out8 is set)
     uint8_t* out8;  // write_color bytes of the f64 colour per packed pixel (nullable)
@@ -893,9 +894,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         y = w / (uint32_t)P->tile_w;
                     }
                     const uint32_t item = slot * tile_px + y * (uint32_t)P->tile_w + x;
-                    const uint32_t tile = (uint32_t)P->rank + slot * (uint32_t)P->world_size;
-                    const uint32_t pi = (tile % (uint32_t)P->tiles_x) * (uint32_t)P->tile_w + x;
-                    const uint32_t pj = (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + y;
+                    const uint32_t pos = (uint32_t)P->rank + slot * (uint32_t)P->world_size;
+                    const uint32_t tile = P->order ? (uint32_t)P->order[pos] : pos;  // -1: empty slot
+                    const uint32_t pi = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu
+                                                            : (tile % (uint32_t)P->tiles_x) * (uint32_t)P->tile_w + x;
+                    const uint32_t pj = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu
+                                                            : (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + y;
                     if (pi >= (uint32_t)cam.image_width || pj >= (uint32_t)cam.image_height) {
                         if (!P->chunk) {  // padding pixel (chunked: gs_combine_kernel writes it)
                             if (P->out) {
@@ -1147,9 +1151,12 @@ __global__ void gs_combine_kernel(const KParams* __restrict__ P) {
     const double scount = 0.0 + (double)P->ss.batch_size;
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < P->capacity; k += gridDim.x * blockDim.x) {
         const uint32_t slot = k / tile_px, w = k % tile_px;
-        const uint32_t tile = (uint32_t)P->rank + slot * (uint32_t)P->world_size;
-        const uint32_t pi = (tile % (uint32_t)P->tiles_x) * (uint32_t)P->tile_w + w % (uint32_t)P->tile_w;
-        const uint32_t pj = (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + w / (uint32_t)P->tile_w;
+        const uint32_t pos = (uint32_t)P->rank + slot * (uint32_t)P->world_size;
+        const uint32_t tile = P->order ? (uint32_t)P->order[pos] : pos;  // -1: empty slot
+        const uint32_t pi = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu
+                                                : (tile % (uint32_t)P->tiles_x) * (uint32_t)P->tile_w + w % (uint32_t)P->tile_w;
+        const uint32_t pj = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu
+                                                : (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + w / (uint32_t)P->tile_w;
         float* o = P->out ? P->out + (size_t)k * 3 : nullptr;
         uint8_t* o8 = P->out8 ? P->out8 + (size_t)k * 3 : nullptr;
         if (pi >= (uint32_t)P->cam.image_width || pj >= (uint32_t)P->cam.image_height) {
@@ -1719,11 +1726,13 @@ gs_status gs_device_scene_destroy(gs_device_scene* ds) {
 
 static bool part_ok(const gs_camera* cam, const gs_partition* p) {
     return cam && p && cam->image_width > 0 && cam->image_height > 0 && p->world_size >= 1 && p->rank >= 0 &&
-           p->rank < p->world_size && p->tile_w > 0 && p->tile_h > 0 && (int64_t)p->tile_w * p->tile_h <= (1 << 20);
+           p->rank < p->world_size && p->tile_w > 0 && p->tile_h > 0 && (int64_t)p->tile_w * p->tile_h <= (1 << 20) &&
+           (!p->d_tile_order || p->slots_per_rank > 0);
 }
 
 int64_t gs_partition_capacity(const gs_camera* cam, const gs_partition* p) {
     if (!part_ok(cam, p)) return -1;
+    if (p->d_tile_order) return (int64_t)p->slots_per_rank * p->tile_w * p->tile_h;
     int64_t tx = (cam->image_width + p->tile_w - 1) / p->tile_w;
     int64_t ty = (cam->image_height + p->tile_h - 1) / p->tile_h;
     int64_t nt = tx * ty;
@@ -1782,6 +1791,7 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     kp.tile_h = part->tile_h;
     kp.tiles_x = (cam->image_width + part->tile_w - 1) / part->tile_w;
     kp.capacity = (uint32_t)cap;
+    kp.order = part->d_tile_order;
     // Split pixels into sample chunks only when the settings run exactly one batch:
     // max_samples < batch_size makes the first stop test (camera.rs:158) always true.
     uint32_t chunk = 0, cpp = 1;
@@ -1915,6 +1925,92 @@ gs_status gs_render(const gs_flat_scene* scene, const gs_camera* cam, const gs_s
     }
     cleanup();
     return r;
+}
+
+gs_status gs_plan_tiles(const gs_device_scene* ds, const gs_camera* cam, uint64_t seed, int32_t world,
+                        int32_t tile_w, int32_t tile_h, int32_t* order_out, int64_t order_cap,
+                        int32_t* slots_per_rank) {
+    if (!ds || !cam || !slots_per_rank || world < 1 || tile_w < 1 || tile_h < 1)
+        return fail(GS_ERR_ARG, "bad argument");
+    gs_partition all{0, 1, tile_w, tile_h, nullptr, 0, 0};
+    if (!part_ok(cam, &all)) return fail(GS_ERR_ARG, "bad partition / image size");
+    const int32_t tx = (cam->image_width + tile_w - 1) / tile_w, ty = (cam->image_height + tile_h - 1) / tile_h;
+    const int32_t nt = tx * ty;
+    const int32_t slots = (nt + world - 1) / world;  // LPT below never gives a rank more (see the cap)
+    if (!order_out) {
+        *slots_per_rank = slots;
+        return GS_OK;
+    }
+    // 1-spp pilot over the whole frame: per-pixel BVH node visits (deterministic).
+    const int64_t cap = gs_partition_capacity(cam, &all);
+    float* d_rgb = nullptr;
+    uint32_t* d_vis = nullptr;
+    if (hipMalloc(&d_rgb, (size_t)cap * 12 + 16) != hipSuccess || hipMalloc(&d_vis, (size_t)cap * 4 + 16) != hipSuccess) {
+        if (d_rgb) (void)hipFree(d_rgb);
+        return fail(GS_ERR_OOM, "hipMalloc failed");
+    }
+    gs_sample_settings one{0.0, 0.0, 1, 0};
+    gs_render_outputs o{d_rgb, nullptr, d_vis};
+    gs_status r = gs_render_tiles_ex_async(ds, cam, &one, seed, &all, &o, nullptr, nullptr);
+    std::vector<uint32_t> vis((size_t)cap);
+    if (r == GS_OK) {
+        hipError_t e = hipDeviceSynchronize();
+        if (e == hipSuccess) e = hipMemcpy(vis.data(), d_vis, (size_t)cap * 4, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) r = fail(GS_ERR_HIP, hipGetErrorString(e));
+    }
+    (void)hipFree(d_rgb);
+    (void)hipFree(d_vis);
+    if (r != GS_OK) return r;
+    // Tile cost: node visits + a per-path constant (shading, camera ray), over real pixels.
+    const int64_t tpx = (int64_t)tile_w * tile_h;
+    std::vector<double> cost(nt, 0.0);
+    for (int32_t t = 0; t < nt; t++) {
+        const int32_t x0 = (t % tx) * tile_w, y0 = (t / tx) * tile_h;
+        for (int32_t y = 0; y < tile_h; y++)
+            for (int32_t x = 0; x < tile_w; x++)
+                if (x0 + x < cam->image_width && y0 + y < cam->image_height)
+                    cost[t] += 16.0 + (double)vis[(size_t)t * tpx + (size_t)y * tile_w + x];
+    }
+    // Longest processing time first: the costliest tile to the least-loaded rank (ties:
+    // lowest rank) among ranks with a free slot.
+    std::vector<int32_t> idx(nt);
+    for (int32_t t = 0; t < nt; t++) idx[t] = t;
+    std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) { return cost[a] > cost[b]; });
+    std::vector<double> load(world, 0.0);
+    std::vector<std::vector<int32_t>> lists(world);
+    for (int32_t t : idx) {
+        int32_t best = -1;
+        for (int32_t rk = 0; rk < world; rk++)
+            if ((int32_t)lists[rk].size() < slots && (best < 0 || load[rk] < load[best])) best = rk;
+        lists[best].push_back(t);
+        load[best] += cost[t];
+    }
+    // Each rank walks its tiles in frame order: measured on MI355X (C4, 8 ranks) frame
+    // order beat descending cost (max rank 87.6 vs 88.0 ms, mean 85.0 vs 86.5): locality
+    // between neighbouring tiles outweighs ending the queue on cheap tiles.
+    for (auto& l : lists) std::sort(l.begin(), l.end());
+    if (order_cap < (int64_t)slots * world) return fail(GS_ERR_ARG, "order_out too small");
+    for (int32_t sl = 0; sl < slots; sl++)
+        for (int32_t rk = 0; rk < world; rk++)
+            order_out[(size_t)sl * world + rk] = sl < (int32_t)lists[rk].size() ? lists[rk][sl] : -1;
+    *slots_per_rank = slots;
+    return GS_OK;
+}
+
+gs_status gs_device_alloc(int64_t bytes, void** d_out) {
+    if (!d_out || bytes < 0) return fail(GS_ERR_ARG, "bad argument");
+    *d_out = nullptr;
+    if (hipMalloc(d_out, (size_t)std::max<int64_t>(bytes, 1)) != hipSuccess) return fail(GS_ERR_OOM, "hipMalloc failed");
+    return GS_OK;
+}
+gs_status gs_device_free(void* d) {
+    if (d) HIPCHK(hipFree(d));
+    return GS_OK;
+}
+gs_status gs_device_upload(void* d_dst, const void* src, int64_t bytes) {
+    if (!d_dst || !src || bytes < 0) return fail(GS_ERR_ARG, "bad argument");
+    HIPCHK(hipMemcpy(d_dst, src, (size_t)bytes, hipMemcpyHostToDevice));
+    return GS_OK;
 }
 
 gs_status gs_render_ppm(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,

@@ -89,18 +89,40 @@ class HostScene:
 class Renderer:
     """A scene resident in HBM of the current device, rendered tile-partitioned."""
 
-    def __init__(self, scene, rank=0, world_size=1, tile=64, tile_h=None):
+    def __init__(self, scene, rank=0, world_size=1, tile=64, tile_h=None, plan=False, plan_seed=1):
+        """plan: cost-balanced tile assignment (gs_plan_tiles: a 1-spp pilot of the whole
+        frame on this device, identical on every rank) instead of round-robin."""
         self.scene = scene
         self.host = HostScene(scene.spec)
         self.cam = camera(scene.camera)
         self.settings = scene.settings
         self.part = N.gs_partition(rank=rank, world_size=world_size, tile_w=tile, tile_h=tile_h or tile)
-        self.capacity = N.lib.gs_partition_capacity(C.byref(self.cam), C.byref(self.part))
-        if self.capacity < 0:
-            raise ValueError("bad partition")
+        self.order = None
+        self.d_order = None
         d = C.c_void_p()
         N.check(N.lib.gs_device_scene_create(self.host.flat_ptr, C.byref(d)))
         self.dev = d
+        if plan:
+            self._plan(plan_seed)
+        self.capacity = N.lib.gs_partition_capacity(C.byref(self.cam), C.byref(self.part))
+        if self.capacity < 0:
+            raise ValueError("bad partition")
+
+    def _plan(self, seed):
+        p = self.part
+        slots = C.c_int32()
+        N.check(N.lib.gs_plan_tiles(self.dev, C.byref(self.cam), seed, p.world_size, p.tile_w, p.tile_h, None, 0,
+                                    C.byref(slots)))
+        order = np.zeros(slots.value * p.world_size, dtype=np.int32)
+        N.check(N.lib.gs_plan_tiles(self.dev, C.byref(self.cam), seed, p.world_size, p.tile_w, p.tile_h,
+                                    order.ctypes.data, order.size, C.byref(slots)))
+        d = C.c_void_p()
+        N.check(N.lib.gs_device_alloc(order.nbytes, C.byref(d)))
+        self.d_order = d
+        N.check(N.lib.gs_device_upload(d, order.ctypes.data, order.nbytes))
+        self.order = order
+        p.d_tile_order = d.value
+        p.slots_per_rank = slots.value
 
     @property
     def width(self):
@@ -124,16 +146,21 @@ class Renderer:
                                                C.c_void_p(stream)))
 
     def unpack_u8_async(self, d_gathered, d_frame, world_size, stream=0):
-        N.check(N.lib.gs_unpack_tiles_u8_async(C.byref(self.cam), world_size, self.part.tile_w, self.part.tile_h,
-                                               self.capacity, C.c_void_p(d_gathered), C.c_void_p(d_frame),
-                                               C.c_void_p(stream)))
+        part = N.gs_partition(0, world_size, self.part.tile_w, self.part.tile_h, self.part.d_tile_order,
+                              self.part.slots_per_rank, 0)
+        N.check(N.lib.gs_unpack_tiles_part_async(C.byref(self.cam), C.byref(part), self.capacity,
+                                                 C.c_void_p(d_gathered), C.c_void_p(d_frame), 3, C.c_void_p(stream)))
 
     def unpack_async(self, d_gathered, d_frame, world_size, stream=0):
-        N.check(N.lib.gs_unpack_tiles_async(C.byref(self.cam), world_size, self.part.tile_w, self.part.tile_h,
-                                            self.capacity, C.c_void_p(d_gathered), C.c_void_p(d_frame),
-                                            C.c_void_p(stream)))
+        part = N.gs_partition(0, world_size, self.part.tile_w, self.part.tile_h, self.part.d_tile_order,
+                              self.part.slots_per_rank, 0)
+        N.check(N.lib.gs_unpack_tiles_part_async(C.byref(self.cam), C.byref(part), self.capacity,
+                                                 C.c_void_p(d_gathered), C.c_void_p(d_frame), 12, C.c_void_p(stream)))
 
     def close(self):
+        if getattr(self, "d_order", None):
+            N.lib.gs_device_free(self.d_order)
+            self.d_order = None
         if getattr(self, "dev", None):
             N.lib.gs_device_scene_destroy(self.dev)
             self.dev = None

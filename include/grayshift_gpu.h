@@ -188,13 +188,20 @@ typedef struct gs_camera {
     double defocus_disk_v[3];
 } gs_camera;
 
-/* Image-space partition: the frame is cut into tile_w x tile_h tiles, tile k goes
- * to rank k mod world_size (round-robin, for load balance under adaptive sampling).
- * A rank's pixels are packed tile after tile, each tile row-major inside, padded to
- * full tiles: packed index = slot*tile_w*tile_h + ty*tile_w + tx. */
+/* Image-space partition: the frame is cut into tile_w x tile_h tiles.  Position
+ * k = slot * world_size + r belongs to rank r; by default position k holds tile k
+ * (round-robin, for load balance under adaptive sampling).  A rank's pixels are packed
+ * slot after slot, each tile row-major inside, padded to full tiles: packed index =
+ * slot*tile_w*tile_h + ty*tile_w + tx.
+ * (ABI 3) d_tile_order, when set, is a DEVICE array of slots_per_rank * world_size tile
+ * ids, position k -> tile (-1: an empty slot), e.g. the cost-balanced plan of
+ * gs_plan_tiles; every tile must appear exactly once. */
 typedef struct gs_partition {
     int32_t rank, world_size;
     int32_t tile_w, tile_h;
+    const int32_t* d_tile_order; /* nullable */
+    int32_t slots_per_rank;      /* with d_tile_order */
+    int32_t pad;
 } gs_partition;
 
 /* Device-resident scene (opaque): uploaded once, rendered many times. */
@@ -286,6 +293,26 @@ gs_status gs_ppm_encode_async(const uint8_t* d_rgb8, int32_t width, int32_t heig
 gs_status gs_render_ppm(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss,
                         uint64_t seed, char* out_text, int64_t text_capacity, int64_t* out_len,
                         gs_counters* counters);
+
+/* Cost-balanced partition (ABI 3): a 1-spp pilot render of the whole frame on this
+ * device (per-pixel BVH node visits, deterministic, so every rank computes the same
+ * plan), then longest-processing-time assignment of tiles to world_size ranks (at
+ * most ceil(tiles / world_size) each), each rank's tiles in frame order.  Writes
+ * order_out (host, world_size * slots entries, see gs_partition.d_tile_order) and
+ * *slots_per_rank; order_cap = entries available (query: order_out NULL, returns the
+ * entries needed in *slots_per_rank * world_size via *slots_per_rank).  Synchronous. */
+gs_status gs_plan_tiles(const gs_device_scene* scene, const gs_camera* cam, uint64_t seed, int32_t world_size,
+                        int32_t tile_w, int32_t tile_h, int32_t* order_out, int64_t order_cap,
+                        int32_t* slots_per_rank);
+
+/* Unpack for any partition (incl. d_tile_order): elem_bytes 12 (f32 rgb) or 3 (rgb8). */
+gs_status gs_unpack_tiles_part_async(const gs_camera* cam, const gs_partition* part, int64_t capacity,
+                                     const void* d_gathered, void* d_frame, int32_t elem_bytes, void* stream);
+
+/* Device memory helpers for callers without their own allocator (ctypes, FFI). */
+gs_status gs_device_alloc(int64_t bytes, void** d_out);
+gs_status gs_device_free(void* d_ptr);
+gs_status gs_device_upload(void* d_dst, const void* host_src, int64_t bytes);
 
 /* Synchronous full-frame render on the current device: upload, render, copy back.
  * out_rgb: host buffer W*H*3 f32 (linear).  counters: host, nullable.  This is the

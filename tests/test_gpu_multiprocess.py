@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, tile, q):
+def _worker(rank, world, port, tile, plan, q):
     import sys
     import ctypes as C
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -37,8 +37,10 @@ def _worker(rank, world, port, tile, q):
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
         sc = scenes.config("C4", width=200, spp=64)
-        r = g.Renderer(sc, rank=rank, world_size=world, tile=tile)
-        cap0 = N.lib.gs_partition_capacity(C.byref(r.cam), C.byref(N.gs_partition(0, world, tile, tile)))
+        r = g.Renderer(sc, rank=rank, world_size=world, tile=tile, plan=plan)
+        # planned partitions give every rank the same capacity; round-robin: rank 0's
+        cap0 = r.capacity if plan else N.lib.gs_partition_capacity(C.byref(r.cam),
+                                                                    C.byref(N.gs_partition(0, world, tile, tile)))
         packed = torch.zeros(cap0 * 3, dtype=torch.float32, device=dev)
         cnt = torch.zeros(16, dtype=torch.int64, device=dev)
         stream = torch.cuda.current_stream(dev).cuda_stream
@@ -65,12 +67,12 @@ def _worker(rank, world, port, tile, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,tile", [(2, 64), (3, 16)])
-def test_ranks_on_gpu_gather_equals_single_rank(world, tile):
+@pytest.mark.parametrize("world,tile,plan", [(2, 64, False), (3, 16, False), (2, 64, True), (3, 32, True)])
+def test_ranks_on_gpu_gather_equals_single_rank(world, tile, plan):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, tile, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, tile, plan, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

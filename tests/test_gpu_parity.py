@@ -167,6 +167,46 @@ def _render_partitioned(sc, world, tile, seed=3):
         n: int(c[i]) for i, n in enumerate(N.COUNTER_NAMES)}
 
 
+def _render_planned(sc, world, tile, seed=3):
+    """gs_plan_tiles partitions: every rank renders its planned tiles, the gathered
+    buffers unpack through the plan's order."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rs = [g.Renderer(sc, rank=r, world_size=world, tile=tile, plan=True) for r in range(world)]
+    cap = rs[0].capacity
+    orders = [r.order for r in rs]
+    for o in orders[1:]:
+        assert np.array_equal(o, orders[0])  # the pilot is deterministic: every rank plans alike
+    tiles = orders[0][orders[0] >= 0]
+    cam = rs[0].cam
+    nt = ((cam.image_width + tile - 1) // tile) * ((cam.image_height + tile - 1) // tile)
+    assert sorted(tiles.tolist()) == list(range(nt))  # each tile exactly once
+    gathered = torch.zeros(world * cap * 3, dtype=torch.float32, device=dev)
+    counters = torch.zeros(16, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for r, rr in enumerate(rs):
+        assert rr.capacity == cap
+        rr.render_async(gathered.data_ptr() + r * cap * 12, counters.data_ptr(), stream, seed=seed)
+    frame = torch.zeros(cam.image_height * cam.image_width * 3, dtype=torch.float32, device=dev)
+    rs[0].unpack_async(gathered.data_ptr(), frame.data_ptr(), world, stream)
+    torch.cuda.synchronize()
+    for rr in rs:
+        rr.close()
+    c = counters.cpu().numpy()
+    return frame.view(cam.image_height, cam.image_width, 3).cpu().numpy(), {
+        n: int(c[i]) for i, n in enumerate(N.COUNTER_NAMES)}
+
+
+@pytest.mark.parametrize("world,tile", [(2, 64), (3, 16), (8, 8)])
+def test_planned_partition_invariance(world, tile):
+    """Cost-balanced tile plans (gs_plan_tiles) change who renders what, never the frame."""
+    sc = scenes.config("C5", width=80, spp=8)
+    full, fc = g.render(sc, seed=3)
+    part, pc = _render_planned(sc, world, tile, seed=3)
+    assert np.array_equal(full, part)
+    assert fc == pc
+
+
 @pytest.mark.parametrize("world,tile", [(1, 64), (2, 64), (3, 16), (4, 24), (8, 8)])
 def test_partition_invariance(world, tile):
     """G logical partitions rendered on one GPU, gathered and unpacked by the device

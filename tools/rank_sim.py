@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--tiles", default="64")
     ap.add_argument("--tile-h", type=int, default=0, help="tile height (default: square tiles)")
+    ap.add_argument("--plan", action="store_true", help="cost-balanced tiles (gs_plan_tiles)")
     a = ap.parse_args()
     import torch
     import grayshift_amd as g
@@ -39,7 +40,7 @@ def main():
             for rank in [int(x) for x in a.ranks.split(",")]:
                 if rank >= world:
                     continue
-                r = g.Renderer(sc, rank=rank, world_size=world, tile=tile, tile_h=a.tile_h or tile)
+                r = g.Renderer(sc, rank=rank, world_size=world, tile=tile, tile_h=a.tile_h or tile, plan=a.plan)
                 out = torch.zeros(r.capacity * 3, dtype=torch.float32, device=dev)
                 cnt = torch.zeros(16, dtype=torch.int64, device=dev)
                 r.render_async(out.data_ptr(), cnt.data_ptr(), stream.cuda_stream, seed=1)  # warm-up
@@ -53,7 +54,7 @@ def main():
                     torch.cuda.synchronize()
                     best = min(best, time.perf_counter() - t0)
                 rays = int(cnt[0].item())
-                print(json.dumps({"world": world, "tile": tile, "rank": rank, "chunk": chunk, "ms": round(best * 1e3, 2),
+                print(json.dumps({"world": world, "tile": tile, "plan": a.plan, "rank": rank, "chunk": chunk, "ms": round(best * 1e3, 2),
                                   "Msamples_per_s": round(rays / best / 1e6, 1)}), flush=True)
                 r.close()
 
