@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_C4_latest.json"),
                     help="JSON with PMC-derived HBM bytes per launch (tools/pmc.sh -> profiles/)")
     ap.add_argument("--dump", default=None, help="write the frame (rank 0) as .npy")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collectives: nccl (= RCCL over xGMI, the measured path) or gloo (host-staged; testing)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="testing only: every rank uses cuda:0 (rehearse N>1 on a one-GPU box; use --backend gloo)")
     return ap.parse_args()
 
 
@@ -71,12 +75,18 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus %d needs torch.distributed.run with %d ranks" % (a.gpus, a.gpus))
+    if a.share_gpu:
+        local = 0
     if local >= torch.cuda.device_count():
         raise SystemExit("rank %d: LOCAL_RANK %d but only %d GPUs visible (one GPU per rank)"
                          % (rank, local, torch.cuda.device_count()))
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    host_coll = world > 1 and a.backend == "gloo"  # gloo collectives on host copies
 
     import grayshift_amd as g
     from grayshift_amd import scenes
@@ -108,7 +118,16 @@ def main():
         ev0.record(stream)
         r.render_async(packed.data_ptr(), counters.data_ptr(), sptr, seed=a.seed)
         ev1.record(stream)
-        if world > 1:
+        if world > 1 and host_coll:
+            src = packed.cpu()
+            if rank == 0:
+                bufs = [torch.empty_like(src) for _ in range(world)]
+                dist.gather(src, gather_list=bufs, dst=0)
+                gathered.copy_(torch.cat(bufs))
+                r.unpack_async(gathered.data_ptr(), frame.data_ptr(), world, sptr)
+            else:
+                dist.gather(src, dst=0)
+        elif world > 1:
             if rank == 0:
                 dist.gather(packed, gather_list=list(gathered.view(world, -1).unbind(0)), dst=0)
                 r.unpack_async(gathered.data_ptr(), frame.data_ptr(), world, sptr)
@@ -141,11 +160,14 @@ def main():
     elapsed = time.perf_counter() - t0
     kms = [e0.elapsed_time(e1) for e0, e1 in kernel_ms]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        cdev = torch.device("cpu") if host_coll else dev
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        km = torch.tensor([sum(kms) / len(kms)], dtype=torch.float64, device=dev)
+        tot_c = tot.to(cdev)
+        dist.all_reduce(tot_c, op=dist.ReduceOp.SUM)
+        tot = tot_c.to(dev)
+        km = torch.tensor([sum(kms) / len(kms)], dtype=torch.float64, device=cdev)
         dist.all_reduce(km, op=dist.ReduceOp.MAX)
         kernel_avg_ms = float(km.item())
     else:

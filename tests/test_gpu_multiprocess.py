@@ -80,3 +80,29 @@ def test_ranks_on_gpu_gather_equals_single_rank(world, tile, plan):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     frame_ok, counters_ok = q.get(timeout=5)
     assert frame_ok and counters_ok
+
+
+def test_bench_two_ranks_shared_gpu(tmp_path):
+    """bench.py's N>1 path end to end (cost-balanced plan, gather, unpack, max-over-ranks
+    timing, one JSON line) rehearsed with 2 ranks on the box's one GPU over gloo: the
+    gathered frame equals the 1-rank frame bit for bit."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["--steps", "1", "--warmup", "1", "--no-cpu", "--width", "160", "--spp", "8"]
+    one = tmp_path / "one.npy"
+    two = tmp_path / "two.npy"
+    r1 = subprocess.run([sys.executable, "bench.py"] + common + ["--dump", str(one)], cwd=root,
+                        capture_output=True, text=True, timeout=300)
+    assert r1.returncode == 0, r1.stderr[-2000:]
+    r2 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+                         "--gpus", "2", "--share-gpu", "--backend", "gloo", "--dump", str(two)] + common,
+                        cwd=root, capture_output=True, text=True, timeout=300)
+    assert r2.returncode == 0, r2.stderr[-2000:]
+    line = [l for l in r2.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["config"]["tile_plan"] == "cost-balanced"
+    assert np.array_equal(np.load(one), np.load(two))
