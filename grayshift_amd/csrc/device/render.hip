@@ -6,18 +6,21 @@
 // BVHNode::hit (BVH.rs:69-90) / AABB::hit (AABB.rs:58-113) / primitive hits →
 // Material::scatter (material.rs) → Texture::value_at / HDRI::sample.
 //
-// Structure (DESIGN.md §4):
-//  * one lane owns one pixel and runs all of its samples in the reference's order,
-//    so the per-pixel sums accumulate exactly as camera.rs:138-147 does;
-//  * a wave pulls pixels from an atomic work queue when lanes finish (ballot +
-//    popcount + one atomicAdd per wave), so sky pixels never wait for busy ones;
+// Structure (DESIGN.md §3.2):
+//  * a lane owns one work item — a pixel, or for single-batch settings a chunk of one
+//    pixel's consecutive samples — and runs its samples in the reference's order, so
+//    the per-pixel sums accumulate exactly as camera.rs:138-147 does (chunk sums are
+//    added in order by gs_combine_kernel);
+//  * a wave hands finished lanes items from its private reserve, refilled by one
+//    atomicAdd of up to 32 items on the global queue, so sky pixels never wait for
+//    busy ones;
 //  * each lane runs a small state machine NEED → TRACE → SHADE → (TRACE | NEED):
 //    the wave keeps stepping BVH traversal until `shade_batch` lanes have finished
 //    their ray, then shades those lanes together (active-ray packing) while the
-//    others keep their traversal state (current ref + LDS stack) for the next round;
+//    others keep their traversal state (one record index) for the next round;
 //  * traversal is the reference's left-first DFS with a global closest-t, restated
-//    as an explicit stack in LDS ([depth][lane], conflict-free), identical in node
-//    visits and primitive tests;
+//    over the tree's pre-order records with hit/miss links (no stack), identical in
+//    node visits and primitive tests; the most-tested records are mirrored in LDS;
 //  * the hit record is recomputed once per ray from (primitive, t) after traversal,
 //    which yields the same values the reference computes at every accepted hit.
 // All arithmetic is f64 with -ffp-contract=off, as the reference's Rust.
@@ -146,10 +149,10 @@ struct KArgs {
 
 enum { S_NEED = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };
 
-// Device-side refs in node children / the root / the traversal stack: a BVH node is its
-// bare index (< 2^26), leaves keep their ABI tag (kind >= 2 in the top 4 bits), and
-// "none" is all ones.  So `cur >= DREF_LEAF` tells a leaf in one compare and a node's
-// byte offset is `cur << 6`.  (Leaf, list and instance records keep ABI refs.)
+// Device-side refs in the two-child node records of BVHs under instances (nested_bvh):
+// a BVH node is its bare index (< 2^26), leaves keep their ABI tag (kind >= 2 in the top
+// 4 bits), and "none" is all ones.  So `cur >= DREF_LEAF` tells a leaf in one compare and
+// a node's byte offset is `cur << 6`.  (Leaf, list and instance records keep ABI refs.)
 #define DREF_NONE 0xFFFFFFFFu
 #define DREF_LEAF (1u << GS_REF_SHIFT)
 __host__ __device__ inline uint32_t device_ref(uint32_t abi_ref) {
