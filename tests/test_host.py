@@ -326,3 +326,31 @@ def test_rust_struct_fields_follow_the_header(name):
     rs_names = re.findall(r"pub ([a-z_0-9]+)\s*:", rs)
     norm = {"min": "mn", "max": "mx"}
     assert [norm.get(n, n) for n in rs_names] == [norm.get(n, n) for n in c_names]
+
+
+# ------------------------------------------------------- tile plans (N > 1)
+def test_planned_partition_capacity_and_validation():
+    cam = g.camera(scenes.config("C4", width=200, spp=1).camera)
+    # with an order table every rank holds slots_per_rank tiles (padded)
+    p = N.gs_partition(1, 4, 64, 64, 0x1000, 3, 0)
+    assert N.lib.gs_partition_capacity(C.byref(cam), C.byref(p)) == 3 * 64 * 64
+    p_bad = N.gs_partition(1, 4, 64, 64, 0x1000, 0, 0)  # an order table needs slots_per_rank > 0
+    assert N.lib.gs_partition_capacity(C.byref(cam), C.byref(p_bad)) == -1
+    rr = N.gs_partition(1, 4, 64, 64, None, 0, 0)       # round-robin: ceil((tiles - rank) / world)
+    tiles = ((200 + 63) // 64) * ((112 + 63) // 64)
+    assert N.lib.gs_partition_capacity(C.byref(cam), C.byref(rr)) == ((tiles - 1 + 3) // 4) * 4096
+
+
+def test_plan_and_device_helpers_reject_bad_arguments_before_the_device():
+    cam = g.camera(scenes.config("C4", width=64, spp=1).camera)
+    slots = C.c_int32()
+    assert N.lib.gs_plan_tiles(None, C.byref(cam), 1, 2, 64, 64, None, 0, C.byref(slots)) == N.GS_ERR_ARG
+    d = C.c_void_p()
+    assert N.lib.gs_device_alloc(-1, C.byref(d)) == N.GS_ERR_ARG
+    assert N.lib.gs_device_upload(None, None, 4) == N.GS_ERR_ARG
+    p = N.gs_partition(0, 2, 64, 64, None, 0, 0)
+    assert N.lib.gs_unpack_tiles_part_async(C.byref(cam), C.byref(p), 4096, C.c_void_p(0x1000),
+                                            C.c_void_p(0x2000), 7, None) == N.GS_ERR_ARG
+    p2 = N.gs_partition(0, 2, 64, 64, 0x1000, 2, 0)  # capacity must match the plan
+    assert N.lib.gs_unpack_tiles_part_async(C.byref(cam), C.byref(p2), 4096, C.c_void_p(0x1000),
+                                            C.c_void_p(0x2000), 12, None) == N.GS_ERR_ARG
