@@ -91,7 +91,7 @@ def main():
     import grayshift_amd as g
     from grayshift_amd import scenes
 
-    g.set_tuning(a.shade_batch or 52, a.blocks_per_cu or 0, 8 if a.leaf_batch is None else a.leaf_batch,
+    g.set_tuning(a.shade_batch or 52, a.blocks_per_cu or 0, 12 if a.leaf_batch is None else a.leaf_batch,
                  -1 if a.sample_chunk is None else a.sample_chunk)
     sc = scenes.config(a.config, width=a.width, spp=a.spp)
     # N > 1: tiles are assigned by a cost-balanced plan computed once at setup (a 1-spp pilot

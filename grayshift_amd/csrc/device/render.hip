@@ -1200,7 +1200,7 @@ __global__ void gs_combine_kernel(const KParams* __restrict__ P) {
 static thread_local std::string tl_err;
 static int32_t g_shade_batch = 52;  // swept on MI355X C4 (chunked, uniform loop): 48 -> 3502, 52 -> 3535-3568, 56 -> 3506-3536 Msamples/s
 static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
-static int32_t g_leaf_batch = 8;
+static int32_t g_leaf_batch = 12;  // swept on MI355X C4 with leaf runs: 8 -> 4586, 10 -> 4632, 12 -> 4648-4651, 14 -> 4624, 16 -> 4592
 // Threaded records mirrored in LDS per block (the shallowest ones): what is left of the
 // block's share of the CU's 160 KiB (4 waves/SIMD = 1024 lanes per CU) after the lane
 // state.  256-lane blocks: 352 records.  -1 = that budget; >= 0 explicit (A/B).
