@@ -137,8 +137,7 @@ struct KParams {
 
 // Hot kernel arguments: what the traversal loop reads every step.
 struct KArgs {
-    const DNode* nodes;
-    const DSphere* spheres;
+    const DNode* nodes;  // the threaded top-level records
     const KParams* P;
     uint32_t root;
     int32_t shade_batch;
@@ -1834,7 +1833,6 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     kp.item_visits = outs->item_visits;
     KArgs a{};
     a.nodes = ds->thr;
-    a.spheres = ds->dev.spheres;
     a.P = ds->params;
     a.root = ds->thr_root;
     a.fast_boxes = ds->fast_boxes ? 1 : 0;
