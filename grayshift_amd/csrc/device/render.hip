@@ -1865,11 +1865,11 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     int64_t max_blocks = ((int64_t)kp.n_items + GS_BLOCK - 1) / GS_BLOCK;
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks < 1) blocks = 1;
-    // Items per queue claim: about 1/64 of a wave's share of the items, at most 32 (a wave
+    // Items per queue claim: about 1/8 of a wave's share of the items, at most 32 (a wave
     // ends holding at most one partly used reserve), at least 1.
     {
         const uint64_t per_wave = (uint64_t)kp.n_items / ((uint64_t)blocks * (GS_BLOCK / 64));
-        kp.claim = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, per_wave / 64));
+        kp.claim = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, per_wave / 8));
     }
     hipLaunchKernelGGL(gs_params_kernel, dim3(1), dim3(64), 0, st, kp, ds->params);
     HIPCHK(hipGetLastError());
