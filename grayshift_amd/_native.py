@@ -184,6 +184,14 @@ class GrayshiftError(RuntimeError):
 def load(path=LIB_PATH):
     if not os.path.exists(path):
         raise ImportError("libgrayshift.so not built (%s): run `python -m grayshift_amd.build`" % path)
+    # One HIP runtime per process: torch wheels bundle their own libamdhip64.so.7 /
+    # libhsa-runtime64.so.1 (same sonames as /opt/rocm's).  Loaded first, they also serve
+    # this library; loaded after /opt/rocm's, torch finds no GPU ("No HIP GPUs are
+    # available").  So bring torch in first when it is installed.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -60,6 +60,7 @@ using namespace gsd;
 // Kernel feature flags (template argument): scenes without them compile the code out.
 #define GS_FEAT_MEDIA 1   // ConstantMedium leaves (RNG draws inside traversal)
 #define GS_FEAT_NESTED 2  // BVHs under Translate/RotateY (a second-level walk, private stack)
+#define GS_FEAT_LEAFRUN 4 // sphere leaves come in adjacent pairs: leaf passes test runs of them
 
 // ---------------------------------------------------------------- device layout
 // Internal layouts (may differ from the ABI records; converted at upload).
@@ -1023,8 +1024,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 // More leaves in the same pass while the next record is a leaf holding a
                 // stationary sphere (the n == 2 leaves of BVH.rs:44-55 sit side by side):
                 // up to GS_LEAF_RUN per pass, each tested in order with the updated closest.
+                // A template feature: trees without such pairs (the Cornell box's quads and
+                // instances) lose ~2% to the loop's mere presence (MI355X C3).
 #pragma unroll 1
-                for (int k = 1; k < GS_LEAF_RUN && cur > THR_END; k++) {
+                for (int k = 1; (FEAT & GS_FEAT_LEAFRUN) && k < GS_LEAF_RUN && cur > THR_END; k++) {
                     const uint32_t l2 = cur & ~THR_LEAF;
                     if (l2 < A.lds_top) {
                         load_leaf_rec_lds(s_top + (l2 << 6), scx, scy, scz, sr, next, ref);
@@ -1501,6 +1504,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     std::vector<DNode> thr;
     std::vector<uint8_t> thr_leaf;
     uint32_t lds_top = 0, thr_root_tagged = THR_END;
+    bool leaf_runs = false;
     {
         // Iterative pre-order: a node pushes a "close" marker below its children, which
         // sets its miss link once its subtree is emitted.
@@ -1590,6 +1594,17 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             placed[pos[i]] = r;
         }
         thr_root_tagged = n == 0 ? THR_END : (thr_leaf[0] ? (THR_LEAF | pos[0]) : pos[0]);
+        // Leaf runs pay when at least a quarter of the leaf records are the first of two
+        // adjacent sphere leaves (C4's two-sphere leaves of BVH.rs:44-55: ~half).
+        {
+            auto is_sph = [&](uint32_t i) { return thr_leaf[i] && (thr[i].right >> GS_REF_SHIFT) == GS_REF_SPHERE; };
+            uint64_t leaves = 0, pairs = 0;
+            for (uint32_t i = 0; i < n; i++) {
+                leaves += thr_leaf[i];
+                pairs += i + 1 < n && is_sph(i) && is_sph(i + 1);
+            }
+            leaf_runs = leaves && pairs * 4 >= leaves;
+        }
         thr.swap(placed);
     }
     if (thr.size() >= (1u << 26)) return fail(GS_ERR_UNSUPPORTED, "more than 2^26 top-level BVH records");
@@ -1709,7 +1724,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ds->thr_root = thr_root_tagged;
     ds->lds_top = lds_top;
     ds->bvh_depth = depth < 1 ? 1 : depth;
-    ds->feat = (s->n_media != 0 ? GS_FEAT_MEDIA : 0) | (nested ? GS_FEAT_NESTED : 0);
+    ds->feat = (s->n_media != 0 ? GS_FEAT_MEDIA : 0) | (nested ? GS_FEAT_NESTED : 0) | (leaf_runs ? GS_FEAT_LEAFRUN : 0);
     ds->fast_boxes = true;
     for (uint32_t i = 0; i < s->n_nodes && ds->fast_boxes; i++)
         for (int k = 0; k < 3; k++)
@@ -1747,6 +1762,11 @@ static void (*kernel_for(int feat))(KArgs) {
         case GS_FEAT_MEDIA: return gs_render_kernel<GS_FEAT_MEDIA>;
         case GS_FEAT_NESTED: return gs_render_kernel<GS_FEAT_NESTED>;
         case GS_FEAT_MEDIA | GS_FEAT_NESTED: return gs_render_kernel<GS_FEAT_MEDIA | GS_FEAT_NESTED>;
+        case GS_FEAT_LEAFRUN: return gs_render_kernel<GS_FEAT_LEAFRUN>;
+        case GS_FEAT_LEAFRUN | GS_FEAT_MEDIA: return gs_render_kernel<GS_FEAT_LEAFRUN | GS_FEAT_MEDIA>;
+        case GS_FEAT_LEAFRUN | GS_FEAT_NESTED: return gs_render_kernel<GS_FEAT_LEAFRUN | GS_FEAT_NESTED>;
+        case GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED:
+            return gs_render_kernel<GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED>;
         default: return gs_render_kernel<0>;
     }
 }
