@@ -354,3 +354,13 @@ def test_plan_and_device_helpers_reject_bad_arguments_before_the_device():
     p2 = N.gs_partition(0, 2, 64, 64, 0x1000, 2, 0)  # capacity must match the plan
     assert N.lib.gs_unpack_tiles_part_async(C.byref(cam), C.byref(p2), 4096, C.c_void_p(0x1000),
                                             C.c_void_p(0x2000), 12, None) == N.GS_ERR_ARG
+
+
+def test_library_shares_torchs_hip_runtime():
+    """_native loads torch before libgrayshift.so so one HIP runtime serves both (torch's
+    bundled libamdhip64.so.7 and /opt/rocm's share a soname; whichever loads first wins)."""
+    import sys
+    assert "torch" in sys.modules
+    maps = open("/proc/self/maps").read()
+    hips = {line.split()[-1] for line in maps.splitlines() if "libamdhip64" in line}
+    assert len(hips) == 1, hips
