@@ -1,34 +1,45 @@
 #!/usr/bin/env python3
 """Benchmark: Msamples/s (primary + secondary rays) of the MI355X megakernel.
 
-Contract (see DESIGN.md §7):
+Contract (see DESIGN.md §4):
     python bench.py --gpus N --steps K --warmup W
 One step = one full frame of the configured workload (default C4: the 10k-sphere
-BVH scene, 1920x1080, 512 spp, HDRI sky), tile-partitioned round-robin over the N
-ranks (64x64 tiles), then one RCCL gather of the finished tiles to rank 0 and an
-unpack into the frame.  The scene is resident in HBM before timing starts.
-value = all rays traced by all ranks / wall time (max over ranks); a "ray" is one
-world.hit call (camera.rs:177), counted on the device by the very launches timed.
+BVH scene, 1920x1080, 512 spp, HDRI sky), tile-partitioned over the N ranks (64x64
+tiles; cost-balanced plan computed on rank 0 and broadcast), then one RCCL gather of
+the finished tiles to rank 0 and an unpack into the frame.  The scene is resident in
+HBM before timing starts.  value = all rays traced by all ranks / wall time (max over
+ranks); a "ray" is one world.hit call (camera.rs:177), counted on the device by the very
+launches timed.
 
-Rank 0 prints ONE JSON line.  At N=1, rank 0 also times the CPU oracle (the
-reference's algorithm restated in C++, oracle/) on a bounded subset of the same
-frame (every --cpu-stride-th row and column, ~10 s): `cpu_baseline`.
+Rank 0 prints ONE JSON line with, beside the contract's fields:
+* parity — the timed frame checked against the CPU oracle (the reference's algorithm
+  restated, oracle/) on a deterministic pixel subset, at the full config;
+* cpu_baseline — at N=1 the oracle's render time on that subset (median of 3, world and
+  BVH build excluded), on this host's cores;
+* roofline — the kernel's binding ceiling, VALU issue, from the PMC summary of this very
+  code object (profiles/pmc/, keyed by the hash of the library's gfx950 code objects),
+  with the measured HBM fraction and the cache-served algorithmic byte rate beside it.
 """
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# Algorithmic bytes per unit (SURVEY.md §8d; DESIGN.md §5): what the reference
-# algorithm reads for each counted event.
+# Algorithmic bytes per unit (SURVEY.md §8d; DESIGN.md §3.3): what the reference
+# algorithm reads for each counted event.  Almost all of it is served from LDS / L1 / L2,
+# so its rate is not an HBM figure.
 BYTES = {"node_visits": 56, "sphere_tests": 40, "msphere_tests": 64, "quad_tests": 136, "tri_tests": 104,
          "instance_tests": 32, "medium_tests": 16, "hits": 32, "image_texels": 3, "hdri_texels": 12, "pixels": 12,
          "noise_evals": 168}  # noise: 7 octaves x 8 corners x 3 permutation-table bytes
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+SIMDS = 1024  # 256 CUs x 4 SIMDs
+VALU_ISSUE_CYCLES = 4  # cycles per wave64 VALU instruction of one wave (f64: half-rate SIMD-32)
+PARITY_TOL = 1e-3  # north star: per-channel |delta| < 1e-3 vs the CPU path at a fixed seed
 
 
 def algorithmic_bytes(c):
@@ -51,14 +62,19 @@ def parse():
     ap.add_argument("--blocks-per-cu", type=int, default=None)
     ap.add_argument("--leaf-batch", type=int, default=None)
     ap.add_argument("--sample-chunk", type=int, default=None, help="samples per work item (-1 auto, 0 whole pixel)")
-    ap.add_argument("--cpu-stride", type=int, default=3, help="CPU baseline: every Nth row and column")
+    ap.add_argument("--cpu-stride", type=int, default=3,
+                    help="CPU baseline / parity subset at N=1: every Nth row and column")
+    ap.add_argument("--parity-stride", type=int, default=12, help="parity subset at N>1: every Nth row and column")
+    ap.add_argument("--cpu-runs", type=int, default=3, help="CPU baseline: median of this many renders")
     ap.add_argument("--cpu-threads", type=int, default=None)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_C4_latest.json"),
-                    help="JSON with PMC-derived HBM bytes per launch (tools/pmc.sh -> profiles/)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and the parity check")
+    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "pmc"),
+                    help="PMC summaries (tools/pmc_summary.py), matched by code-object hash and config")
     ap.add_argument("--dump", default=None, help="write the frame (rank 0) as .npy")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collectives: nccl (= RCCL over xGMI, the measured path) or gloo (host-staged; testing)")
+    ap.add_argument("--gather", action="store_true",
+                    help="run the gather path even at N=1 (a 1-rank process group; exercises RCCL on one GPU)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="testing only: every rank uses cuda:0 (rehearse N>1 on a one-GPU box; use --backend gloo)")
     return ap.parse_args()
@@ -66,27 +82,31 @@ def parse():
 
 def main():
     a = parse()
+    import numpy as np
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("--gpus %d needs torch.distributed.run with %d ranks" % (a.gpus, a.gpus))
+    if world != a.gpus and world == 1 and a.gpus > 1:
+        raise SystemExit("--gpus %d needs torch.distributed.run with %d ranks" % (a.gpus, a.gpus))
     if a.share_gpu:
         local = 0
     if local >= torch.cuda.device_count():
         raise SystemExit("rank %d: LOCAL_RANK %d but only %d GPUs visible (one GPU per rank)"
                          % (rank, local, torch.cuda.device_count()))
     torch.cuda.set_device(local)
-    if world > 1:
+    dev = torch.device("cuda", local)
+    use_pg = world > 1 or a.gather
+    if use_pg:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
         if a.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
-            dist.init_process_group("gloo")
-    host_coll = world > 1 and a.backend == "gloo"  # gloo collectives on host copies
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+    host_coll = use_pg and a.backend == "gloo"  # gloo collectives on host copies
 
     import grayshift_amd as g
     from grayshift_amd import scenes
@@ -94,18 +114,33 @@ def main():
     g.set_tuning(a.shade_batch or 52, a.blocks_per_cu or 0, 12 if a.leaf_batch is None else a.leaf_batch,
                  -1 if a.sample_chunk is None else a.sample_chunk)
     sc = scenes.config(a.config, width=a.width, spp=a.spp)
-    # N > 1: tiles are assigned by a cost-balanced plan computed once at setup (a 1-spp pilot
-    # of the frame, identical on every rank; outside the timed region, like the BVH build).
+    # N > 1: tiles are assigned by a cost-balanced plan (a 1-spp pilot of the frame),
+    # computed once at setup on rank 0 and broadcast, so every rank uses the same one
+    # (outside the timed region, like the BVH build).
     plan = world > 1 and not a.no_plan
-    r = g.Renderer(sc, rank=rank, world_size=world, tile=a.tile, plan=plan)
+    order = None
+    if plan:
+        cam = g.camera(sc.camera)
+        tiles = -(-cam.image_width // a.tile) * -(-cam.image_height // a.tile)
+        slots = -(-tiles // world)  # gs_plan_tiles: at most ceil(tiles / world) per rank
+        r = g.Renderer(sc, rank=rank, world_size=world, tile=a.tile, plan=True) if rank == 0 else None
+        cdev = torch.device("cpu") if host_coll else dev
+        t = torch.from_numpy(r.order).to(cdev) if rank == 0 else \
+            torch.empty(slots * world, dtype=torch.int32, device=cdev)
+        dist.broadcast(t, src=0)
+        order = t.cpu().numpy()
+        if rank != 0:
+            r = g.Renderer(sc, rank=rank, world_size=world, tile=a.tile, order=order)
+    else:
+        r = g.Renderer(sc, rank=rank, world_size=world, tile=a.tile)
     # Every rank's packed buffer has rank 0's capacity (the most tiles any rank holds)
+    import ctypes as C
     p0 = g._native.gs_partition(0, world, a.tile, a.tile, r.part.d_tile_order, r.part.slots_per_rank, 0)
-    cap0 = g._native.lib.gs_partition_capacity(__import__("ctypes").byref(r.cam), __import__("ctypes").byref(p0))
-    dev = torch.device("cuda", local)
+    cap0 = g._native.lib.gs_partition_capacity(C.byref(r.cam), C.byref(p0))
     packed = torch.zeros(cap0 * 3, dtype=torch.float32, device=dev)
     counters = torch.zeros(16, dtype=torch.int64, device=dev)
     frame = torch.zeros(r.height * r.width * 3, dtype=torch.float32, device=dev) if rank == 0 else None
-    gathered = torch.empty(world * cap0 * 3, dtype=torch.float32, device=dev) if (rank == 0 and world > 1) else None
+    gathered = torch.empty(world * cap0 * 3, dtype=torch.float32, device=dev) if (rank == 0 and use_pg) else None
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
@@ -118,7 +153,7 @@ def main():
         ev0.record(stream)
         r.render_async(packed.data_ptr(), counters.data_ptr(), sptr, seed=a.seed)
         ev1.record(stream)
-        if world > 1 and host_coll:
+        if host_coll:
             src = packed.cpu()
             if rank == 0:
                 bufs = [torch.empty_like(src) for _ in range(world)]
@@ -127,7 +162,7 @@ def main():
                 r.unpack_async(gathered.data_ptr(), frame.data_ptr(), world, sptr)
             else:
                 dist.gather(src, dst=0)
-        elif world > 1:
+        elif use_pg:  # RCCL over xGMI
             if rank == 0:
                 dist.gather(packed, gather_list=list(gathered.view(world, -1).unbind(0)), dst=0)
                 r.unpack_async(gathered.data_ptr(), frame.data_ptr(), world, sptr)
@@ -146,7 +181,7 @@ def main():
         tot += counters
     torch.cuda.synchronize()
     tot.zero_()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -154,12 +189,12 @@ def main():
         step(True)
         tot += counters
     torch.cuda.synchronize()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kms = [e0.elapsed_time(e1) for e0, e1 in kernel_ms]
-    if world > 1:
+    if use_pg:
         cdev = torch.device("cpu") if host_coll else dev
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -177,24 +212,17 @@ def main():
     c = {n: int(tot[i].item()) // a.steps for i, n in enumerate(COUNTER_NAMES)}
     rays_per_frame = c["rays"]
     value = rays_per_frame * a.steps / elapsed / 1e6
-    abytes = algorithmic_bytes(c) / max(1, world)  # per launch (per rank)
-    achieved = abytes / (kernel_avg_ms / 1e3) / 1e9
-
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(sc, a)
-
-    traffic = None
-    if a.traffic and os.path.exists(a.traffic) and world == 1:  # a 1-GPU whole-frame figure
-        with open(a.traffic) as f:
-            tj = json.load(f)
-        if tj.get("config") == a.config and tj.get("hbm_bytes_per_launch") and a.width is None and a.spp is None:
-            traffic = tj["hbm_bytes_per_launch"]
 
     if rank == 0:
+        img = frame.view(r.height, r.width, 3).cpu().numpy()
         if a.dump:
-            import numpy as np
-            np.save(a.dump, frame.view(r.height, r.width, 3).cpu().numpy())
+            np.save(a.dump, img)
+        cpu = parity = None
+        if not a.no_cpu:
+            stride = a.cpu_stride if world == 1 else a.parity_stride
+            cpu, parity = cpu_check(sc, a, img, stride, runs=a.cpu_runs if world == 1 else 1)
+            if world > 1:
+                cpu = None  # the CPU baseline is an N=1 figure
         invalid = a.width is not None or a.spp is not None
         out = {
             "metric": "Msamples/sec (primary+secondary rays)",
@@ -213,38 +241,97 @@ def main():
                 "workload": "%s: %s %dx%d, %d spp%s" % (a.config, sc.name, r.width, r.height,
                                                       sc.settings.batch_size,
                                                       " (OVERRIDDEN: not the metric)" if invalid else ""),
-                "tile": a.tile, "parallelism": "tiles%d" % world, "tile_plan": "cost-balanced" if plan else "round-robin",
+                "tile": a.tile, "parallelism": "tiles%d" % world,
+                "tile_plan": "cost-balanced" if plan else "round-robin",
+                "collective": ("rccl" if a.backend == "nccl" else "gloo") if use_pg else "none",
                 "seed": a.seed,
                 "rays_per_frame": rays_per_frame, "paths_per_frame": c["paths"],
                 "node_visits_per_ray": round(c["node_visits"] / max(1, rays_per_frame), 3),
             },
-            "roofline": {
-                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel_ms": round(kernel_avg_ms, 3), "algorithmic_bytes_per_launch": int(abytes),
-            },
+            "roofline": roofline(a, c, world, kernel_avg_ms, invalid),
+            "parity": parity,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
     r.close()
 
 
-def cpu_baseline(sc, a):
-    """The CPU oracle on every cpu_stride-th row and column of the same frame."""
+def roofline(a, c, world, kernel_ms, invalid):
+    """The dominant kernel's ceiling.  The C4 working set (~3.5 MB: threaded BVH records
+    and the RGBE sky) lives in LDS / L1 / L2, so HBM does not bound it (measured fabric
+    traffic below); VALU issue does.  frac = VALU wave-instructions x 4 cycles over the
+    SIMDs' cycles, from the PMC summary of this very code object (same config), with the
+    instruction rate taken over this run's kernel time."""
+    from grayshift_amd import codeobj
+    from grayshift_amd._native import LIB_PATH
+    kernel_s = kernel_ms / 1e3
+    abytes = algorithmic_bytes(c) / max(1, world)  # per launch (per rank)
+    out = {"bound": "valu_issue", "achieved": None, "peak": None, "unit": "G VALU wave-instr/s", "frac": None,
+           "traffic": None, "hbm_frac": None, "kernel_ms": round(kernel_ms, 3),
+           "cache_served_algorithmic_GBps": round(abytes / kernel_s / 1e9, 1),
+           "cache_served_algorithmic_over_hbm_peak": round(abytes / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
+           "algorithmic_bytes_per_launch": int(abytes), "pmc": None}
+    try:
+        h = codeobj.code_object_hash(LIB_PATH)
+    except Exception as e:  # noqa: BLE001
+        out["pmc"] = "no code-object hash: %s" % e
+        return out
+    out["code_object"] = h
+    if invalid or world != 1:
+        return out  # the PMC summaries are 1-GPU whole-frame figures of the metric's config
+    path = os.path.join(a.pmc_dir, "%s_%s.json" % (a.config, h))
+    if not os.path.exists(path):
+        out["pmc"] = "none for this code object (%s)" % os.path.relpath(path, ROOT)
+        return out
+    pj = json.load(open(path))
+    k = pj["counters"]
+    prof_s = pj["kernel_duration_ms_profiled"] / 1e3
+    clock = k["GRBM_GUI_ACTIVE"] / 8.0 / prof_s  # effective shader clock of the profiled launch (Hz)
+    achieved = k["SQ_INSTS_VALU"] / kernel_s
+    peak = SIMDS * clock / VALU_ISSUE_CYCLES
+    out.update({"achieved": round(achieved / 1e9, 2), "peak": round(peak / 1e9, 2), "frac": round(achieved / peak, 4),
+                "traffic": pj["hbm_bytes_per_launch"],
+                "hbm_frac": round(pj["hbm_bytes_per_launch"] / kernel_s / 1e9 / HBM_PEAK_GBS, 5),
+                "effective_clock_ghz": round(clock / 1e9, 3),
+                "valu_busy_frac_pmc": round(k["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * k["GRBM_GUI_ACTIVE"] / 8.0), 4)
+                if "SQ_ACTIVE_INST_VALU" in k else None,
+                "pmc": os.path.relpath(path, ROOT)})
+    return out
+
+
+def cpu_check(sc, a, img, stride, runs):
+    """The CPU oracle on every stride-th row and column of the same frame: its render time
+    (median of `runs`; world/BVH build excluded) and the per-channel parity of the GPU
+    frame at those pixels."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle  # test-infrastructure checker, used here only as the CPU baseline
+    import oracle  # test-infrastructure checker, used here as the checker and the CPU baseline only
     threads = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    W, H, s = sc.width, sc.height, a.cpu_stride
-    sub = np.array([j * W + i for j in range(0, H, s) for i in range(0, W, s)], dtype=np.int32)
-    t0 = time.perf_counter()
-    _, c = oracle.render(sc, seed=a.seed, threads=threads, subset=sub)
-    dt = time.perf_counter() - t0
-    return {"value": round(c["rays"] / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": "%d px (every %dth row/col of the frame) x %d spp = %d rays in %.1fs (incl. world/BVH build)"
-                      % (len(sub), s, sc.settings.batch_size, c["rays"], dt)}
+    W, H = sc.width, sc.height
+    sub = np.array([j * W + i for j in range(0, H, stride) for i in range(0, W, stride)], dtype=np.int32)
+    times, ref, cnt = [], None, None
+    for _ in range(max(1, runs)):
+        tm = {}
+        rgb, cc = oracle.render(sc, seed=a.seed, threads=threads, subset=sub, timing=tm)
+        times.append(tm["render_s"])
+        if ref is None:
+            ref, cnt = rgb, cc
+        elif not np.array_equal(ref, rgb):
+            raise RuntimeError("CPU oracle is not deterministic across runs")
+    med = statistics.median(times)
+    gpu = img.reshape(-1, 3)[sub].astype(np.float64)
+    d = np.abs(gpu - ref.astype(np.float64))
+    parity = {"pixels": int(len(sub)), "subset": "every %dth row and column" % stride,
+              "max_abs_delta": float(d.max()), "n_over_tol": int((d >= PARITY_TOL).sum()), "tolerance": PARITY_TOL,
+              "bit_identical_frac": round(float((gpu == ref.astype(np.float64)).mean()), 6),
+              "pass": bool(d.max() < PARITY_TOL)}
+    cpu = {"value": round(cnt["rays"] / med / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "sample": "%d px (every %dth row/col of the frame) x %d spp = %d rays; render only (world/BVH build "
+                     "excluded), median of %d: %s s" % (len(sub), stride, sc.settings.batch_size, cnt["rays"],
+                                                        len(times), ", ".join("%.2f" % t for t in times))}
+    return cpu, parity
 
 
 if __name__ == "__main__":

@@ -13,9 +13,10 @@ import importlib
 _EXPORTS = {
     "HostScene": "renderer", "Renderer": "renderer", "camera": "renderer", "render": "renderer",
     "set_tuning": "renderer", "write_ppm": "renderer", "render_ppm": "renderer", "ppm_encode_async": "renderer",
+    "render_multi": "renderer",
     "SceneBuilder": "scene", "camera_spec": "scene", "fixed_spp": "scene", "sample_settings": "scene",
 }
-_SUBMODULES = {"scenes", "partition", "assets", "_native", "scene"}
+_SUBMODULES = {"scenes", "partition", "assets", "_native", "scene", "codeobj"}
 
 __all__ = sorted(_EXPORTS) + ["scenes"]
 

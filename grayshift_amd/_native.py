@@ -16,7 +16,7 @@ GS_OBJ_LIST, GS_OBJ_BVH, GS_OBJ_TRANSLATE, GS_OBJ_ROTATE_Y, GS_OBJ_CUBE, GS_OBJ_
 GS_MAT_LAMBERTIAN, GS_MAT_METAL, GS_MAT_DIELECTRIC, GS_MAT_DIFFUSE_LIGHT, GS_MAT_ISOTROPIC = 1, 2, 3, 4, 5
 GS_TEX_SOLID, GS_TEX_CHECKERED, GS_TEX_IMAGE, GS_TEX_NOISE = 1, 2, 3, 4
 GS_BG_SOLID, GS_BG_HDRI = 1, 2
-GS_ABI_VERSION = 3
+GS_ABI_VERSION = 4
 GS_OK, GS_ERR_ARG, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPORTED, GS_ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5
 
 D3 = C.c_double * 3
@@ -123,6 +123,23 @@ class gs_render_outputs(C.Structure):
     _fields_ = [("rgb", C.c_void_p), ("rgb8", C.c_void_p), ("item_visits", C.c_void_p)]
 
 
+class gs_launch(C.Structure):
+    _fields_ = [("num_gpus", C.c_int32), ("tile_w", C.c_int32), ("tile_h", C.c_int32), ("plan", C.c_int32),
+                ("devices", C.c_void_p)]
+
+
+class gs_multi_outputs(C.Structure):
+    _fields_ = [("rgb", C.c_void_p), ("rgb8", C.c_void_p), ("ppm_text", C.c_void_p), ("ppm_capacity", C.c_int64),
+                ("ppm_len", C.POINTER(C.c_int64))]
+
+
+class gs_stats(C.Structure):
+    _fields_ = [("counters", gs_counters), ("setup_ms", C.c_double), ("total_ms", C.c_double),
+                ("render_ms_max", C.c_double), ("render_ms_min", C.c_double), ("gather_ms", C.c_double),
+                ("algorithmic_bytes", C.c_uint64), ("gathered_bytes", C.c_uint64), ("num_gpus", C.c_int32),
+                ("pad", C.c_int32)]
+
+
 # Every symbol include/*.h declares, with its ctypes signature.
 _P = C.c_void_p
 SIGNATURES = {
@@ -130,6 +147,7 @@ SIGNATURES = {
     "gs_last_error": (C.c_char_p, []),
     "gs_version": (C.c_int32, []),
     "gs_set_tuning": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
+    "gs_debug_set_partial_budget": (C.c_int32, [C.c_uint64]),
     "gs_device_scene_create": (C.c_int32, [_P, C.POINTER(_P)]),
     "gs_device_scene_destroy": (C.c_int32, [_P]),
     "gs_partition_capacity": (C.c_int64, [C.POINTER(gs_camera), C.POINTER(gs_partition)]),
@@ -157,6 +175,9 @@ SIGNATURES = {
     "gs_device_upload": (C.c_int32, [_P, _P, C.c_int64]),
     "gs_render": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64, _P,
                               C.POINTER(gs_counters)]),
+    "gs_render_multi": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64,
+                                    C.POINTER(gs_launch), C.POINTER(gs_multi_outputs), C.POINTER(gs_stats)]),
+    "gs_rccl_library": (C.c_char_p, []),
     # grayshift_host.h
     "gs_host_scene_from_spec": (C.c_int32, [C.POINTER(gs_scene_spec), C.POINTER(_P)]),
     "gs_host_scene_destroy": (C.c_int32, [_P]),
@@ -181,17 +202,30 @@ class GrayshiftError(RuntimeError):
         self.code = code
 
 
+def _preload_hip_runtime():
+    """One HIP runtime per process.  torch wheels bundle their own libamdhip64.so.7 /
+    libhsa-runtime64 (the same sonames as /opt/rocm's).  Loaded first, they also serve
+    this library; if /opt/rocm's were loaded first, a later `import torch` would find no
+    GPU ("No HIP GPUs are available").  So when torch is installed, load torch's HIP
+    runtime library (by path: no `import torch`, so importing this package stays cheap)
+    before this library; without torch, /opt/rocm's is used."""
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.submodule_search_locations:
+        return None
+    hip = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if not os.path.exists(hip):
+        return None
+    return C.CDLL(hip, mode=C.RTLD_GLOBAL)
+
+
 def load(path=LIB_PATH):
     if not os.path.exists(path):
         raise ImportError("libgrayshift.so not built (%s): run `python -m grayshift_amd.build`" % path)
-    # One HIP runtime per process: torch wheels bundle their own libamdhip64.so.7 /
-    # libhsa-runtime64.so.1 (same sonames as /opt/rocm's).  Loaded first, they also serve
-    # this library; loaded after /opt/rocm's, torch finds no GPU ("No HIP GPUs are
-    # available").  So bring torch in first when it is installed.
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    _preload_hip_runtime()
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

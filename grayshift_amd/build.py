@@ -27,6 +27,7 @@ SOURCES = [
     os.path.join(HERE, "csrc", "host", "world.cpp"),
     os.path.join(HERE, "csrc", "host", "camera.cpp"),
     os.path.join(HERE, "csrc", "host", "host_capi.cpp"),
+    os.path.join(HERE, "csrc", "host", "multi_gpu.cpp"),
 ]
 DEPS = SOURCES + [
     os.path.join(HERE, "csrc", "device", "devmath.hpp"),
@@ -74,7 +75,7 @@ def build_product(force=False, verbose=False, extra=(), out=None):
         subprocess.run(cmd, check=True)
         objs.append(obj)
     tmp = lib + ".tmp"
-    cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", tmp] + objs + ["-lpthread"]
+    cmd = [HIPCC, "-shared", "--offload-arch=" + ARCH, "-o", tmp] + objs + ["-lpthread", "-ldl"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -1220,7 +1220,7 @@ static uint32_t lds_top_budget() {
 // 16 -> 648.3, 32 -> 647.3; N=8: 4 -> 89.6, 8 -> 89.6, 16 -> 89.7, 32 -> 95.8 (max of the
 // two ranks).  16 is within noise of the best at both ends.
 static int32_t g_sample_chunk = -1;
-static const uint64_t kPartialBudget = 4ull << 30;  // auto chunks: at most 4 GiB of chunk sums
+static uint64_t g_partial_budget = 4ull << 30;  // auto chunks: at most 4 GiB of chunk sums (per launch slot)
 
 extern "C" void gs_set_last_error(const char* msg) { tl_err = msg ? msg : ""; }
 static gs_status fail(gs_status code, const std::string& msg) {
@@ -1233,12 +1233,24 @@ static gs_status fail(gs_status code, const std::string& msg) {
         if (e_ != hipSuccess) return fail(GS_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// One in-flight launch's device state: its parameter block, its work-queue counter and
+// its chunk sums.  A scene keeps a small ring of them, so launches of one scene on
+// different streams (or host threads) never share state; a slot is reused only after
+// the stream of the new launch has waited for the slot's previous launch (its event).
+struct LaunchSlot {
+    KParams* params = nullptr;  // device
+    uint32_t* queue = nullptr;  // device
+    double* partial = nullptr;  // chunk partial sums, grown on demand
+    size_t partial_bytes = 0;
+    hipEvent_t done = nullptr;  // recorded after the slot's last launch
+    bool used = false;
+};
+static const int kLaunchSlots = 4;
+
 struct gs_device_scene {
     int device = 0;
     void* mem = nullptr;  // one allocation for every array
     size_t bytes = 0;
-    uint32_t* queue = nullptr;
-    KParams* params = nullptr;  // per-launch cold parameters (device memory)
     DevScene dev{};
     uint32_t n_nodes = 0;
     uint32_t bvh_depth = 1;  // top-level BVH depth (informational: the walk keeps no stack)
@@ -1247,13 +1259,15 @@ struct gs_device_scene {
     const DNode* thr = nullptr;  // threaded top-level records (THR_END)
     uint32_t thr_root = THR_END;
     uint32_t lds_top = 0;        // records mirrored in LDS per block
+    // Launch state, mutated by launches of a const scene: guarded by `mu`.
+    std::mutex mu;
     // launch geometry, computed at the first launch (host API queries cost ~0.5 ms each)
     bool launch_ready = false;
     int cus = 0, per_cu = 0;
     uint32_t launch_lds_top = 0;
     size_t launch_lds = 0;
-    double* partial = nullptr;  // chunk partial sums, grown on demand
-    size_t partial_bytes = 0;
+    LaunchSlot slots[kLaunchSlots];
+    uint32_t next_slot = 0;
 };
 
 namespace {
@@ -1483,6 +1497,11 @@ gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf
     return GS_OK;
 }
 
+gs_status gs_debug_set_partial_budget(uint64_t bytes) {
+    g_partial_budget = bytes ? bytes : (4ull << 30);
+    return GS_OK;
+}
+
 gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) {
     if (!s || !out) return fail(GS_ERR_ARG, "null argument");
     *out = nullptr;
@@ -1680,8 +1699,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     size_t o_texel = L.add(s->texels8, s->n_texels8);
     size_t o_hdri = L.add(s->hdri_rgb, (s->background.kind == GS_BG_HDRI && rgbe.empty()) ? s->n_hdri_floats * 4 : 0);
     size_t o_rgbe = L.add(rgbe.data(), rgbe.size() * 4);
-    size_t o_queue = L.add(nullptr, 64);
-    size_t o_params = L.add(nullptr, sizeof(KParams));
+    size_t o_slot[kLaunchSlots];
+    for (int k = 0; k < kLaunchSlots; k++) o_slot[k] = L.add(nullptr, 256 + sizeof(KParams));  // queue, params
 
     auto ds = new gs_device_scene();
     (void)hipGetDevice(&ds->device);
@@ -1717,8 +1736,14 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     d.hdri_rgbe = rgbe.empty() ? nullptr : (const uint32_t*)(b + o_rgbe);
     d.bg = s->background;
     d.root = device_ref(s->root);
-    ds->queue = (uint32_t*)(b + o_queue);
-    ds->params = (KParams*)(b + o_params);
+    for (int k = 0; k < kLaunchSlots; k++) {
+        ds->slots[k].queue = (uint32_t*)(b + o_slot[k]);
+        ds->slots[k].params = (KParams*)(b + o_slot[k] + 256);
+        if (hipEventCreateWithFlags(&ds->slots[k].done, hipEventDisableTiming) != hipSuccess) {
+            gs_device_scene_destroy(ds);
+            return fail(GS_ERR_HIP, "hipEventCreateWithFlags failed");
+        }
+    }
     ds->n_nodes = s->n_nodes;
     ds->thr = (const DNode*)(b + o_thr);
     ds->thr_root = thr_root_tagged;
@@ -1735,8 +1760,14 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
 
 gs_status gs_device_scene_destroy(gs_device_scene* ds) {
     if (!ds) return GS_OK;
+    for (auto& sl : ds->slots) {
+        if (sl.done) {
+            if (sl.used) (void)hipEventSynchronize(sl.done);
+            (void)hipEventDestroy(sl.done);
+        }
+        if (sl.partial) (void)hipFree(sl.partial);
+    }
     if (ds->mem) (void)hipFree(ds->mem);
-    if (ds->partial) (void)hipFree(ds->partial);
     delete ds;
     return GS_OK;
 }
@@ -1822,7 +1853,7 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
         uint32_t c = g_sample_chunk > 0 ? (uint32_t)g_sample_chunk : std::max<uint32_t>(16u, (bs + 63u) / 64u);
         if ((bs + c - 1) / c > 64u) c = (bs + 63u) / 64u;  // at most 64 chunks per pixel
         if (g_sample_chunk < 0)
-            while (c < bs && (uint64_t)cap * ((bs + c - 1) / c) * 24u > kPartialBudget) c *= 2u;
+            while (c < bs && (uint64_t)cap * ((bs + c - 1) / c) * 24u > g_partial_budget) c *= 2u;
         if (c < bs) {
             chunk = c;
             cpp = (bs + c - 1) / c;
@@ -1833,32 +1864,18 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     kp.cpp = cpp;
     kp.n_items = (uint32_t)cap * cpp;
     kp.claim = 1;  // set below, once the grid size is known
-    if (chunk) {
-        const size_t need = (size_t)kp.n_items * 3 * sizeof(double);
-        gs_device_scene* mds = const_cast<gs_device_scene*>(ds);
-        if (mds->partial_bytes < need) {
-            if (mds->partial) (void)hipFree(mds->partial);  // synchronises: no launch still reads it
-            mds->partial = nullptr;
-            mds->partial_bytes = 0;
-            if (hipMalloc(&mds->partial, need) != hipSuccess)
-                return fail(GS_ERR_OOM, "hipMalloc of " + std::to_string(need) + " bytes of chunk sums failed");
-            mds->partial_bytes = need;
-        }
-        kp.partial = mds->partial;
-    }
     kp.out = outs->rgb;
     kp.out8 = outs->rgb8;
     kp.counters = (unsigned long long*)d_counters;
-    kp.queue = ds->queue;
     kp.item_visits = outs->item_visits;
     KArgs a{};
     a.nodes = ds->thr;
-    a.P = ds->params;
     a.root = ds->thr_root;
     a.fast_boxes = ds->fast_boxes ? 1 : 0;
     a.shade_batch = g_shade_batch;
     a.leaf_batch = g_leaf_batch < 1 ? 1 : g_leaf_batch;  // 0 would never step a node
     gs_device_scene* mds = const_cast<gs_device_scene*>(ds);
+    std::lock_guard<std::mutex> lock(mds->mu);
     if (!mds->launch_ready) {
         HIPCHK(hipDeviceGetAttribute(&mds->cus, hipDeviceAttributeMultiprocessorCount, dev));
         // The mirror takes what the block's LDS limit leaves after the kernel's static LDS
@@ -1887,20 +1904,44 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     if (blocks < 1) blocks = 1;
     // Items per queue claim: about 1/8 of a wave's share of the items, at most 32 (a wave
     // ends holding at most one partly used reserve), at least 1.
-    {
-        const uint64_t per_wave = (uint64_t)kp.n_items / ((uint64_t)blocks * (GS_BLOCK / 64));
-        kp.claim = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, per_wave / 8));
+    const uint64_t waves = (uint64_t)blocks * (GS_BLOCK / 64);
+    kp.claim = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, (uint64_t)kp.n_items / waves / 8));
+    // The u32 queue counter runs past n_items by at most one claim per wave (each wave's
+    // last, failed claim): it must not wrap.
+    if ((uint64_t)kp.n_items + (uint64_t)kp.claim * (waves + 1) >= 0xFFFFFFFFull)
+        return fail(GS_ERR_ARG, "too many work items for the 32-bit work queue");
+
+    // This launch's slot: wait (on `st`) for the slot's previous launch before reusing it.
+    LaunchSlot& sl = mds->slots[mds->next_slot++ % kLaunchSlots];
+    if (sl.used) HIPCHK(hipStreamWaitEvent(st, sl.done, 0));
+    if (chunk) {
+        const size_t need = (size_t)kp.n_items * 3 * sizeof(double);
+        if (sl.partial_bytes < need) {
+            if (sl.used) HIPCHK(hipEventSynchronize(sl.done));  // nothing in flight reads it
+            if (sl.partial) (void)hipFree(sl.partial);
+            sl.partial = nullptr;
+            sl.partial_bytes = 0;
+            if (hipMalloc(&sl.partial, need) != hipSuccess)
+                return fail(GS_ERR_OOM, "hipMalloc of " + std::to_string(need) + " bytes of chunk sums failed");
+            sl.partial_bytes = need;
+        }
+        kp.partial = sl.partial;
     }
-    hipLaunchKernelGGL(gs_params_kernel, dim3(1), dim3(64), 0, st, kp, ds->params);
+    kp.queue = sl.queue;
+    a.P = sl.params;
+    if (outs->item_visits) HIPCHK(hipMemsetAsync(outs->item_visits, 0, (size_t)cap * sizeof(uint32_t), st));
+    hipLaunchKernelGGL(gs_params_kernel, dim3(1), dim3(64), 0, st, kp, sl.params);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemsetAsync(ds->queue, 0, 4, st));
+    HIPCHK(hipMemsetAsync(sl.queue, 0, 4, st));
     hipLaunchKernelGGL(kernel_for(ds->feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
     if (chunk) {
         const unsigned grid = (unsigned)std::min<int64_t>((cap + 255) / 256, 8192);
-        hipLaunchKernelGGL(gs_combine_kernel, dim3(grid), dim3(256), 0, st, (const KParams*)ds->params);
+        hipLaunchKernelGGL(gs_combine_kernel, dim3(grid), dim3(256), 0, st, (const KParams*)sl.params);
         HIPCHK(hipGetLastError());
     }
+    HIPCHK(hipEventRecord(sl.done, st));
+    sl.used = true;
     return GS_OK;
 }
 

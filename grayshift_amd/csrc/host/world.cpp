@@ -130,58 +130,58 @@ static void check_index(size_t n, const char* what) {
 }
 
 uint32_t Flattener::material_index(const Material* m) {
-    for (size_t i = 0; i < mat_keys.size(); i++)
-        if (mat_keys[i] == m) return (uint32_t)i;
+    auto it = mat_slot.find(m);
+    if (it != mat_slot.end()) return it->second;
     // Reserve the slot first so recursive texture flattening cannot reorder it.
-    mat_keys.push_back(m);
+    const uint32_t idx = (uint32_t)materials.size();
+    mat_slot.emplace(m, idx);
     materials.push_back(gs_material{});
-    uint32_t idx = (uint32_t)(materials.size() - 1);
     m->flatten(*this);  // fills materials[idx]
     return idx;
 }
 uint32_t Flattener::texture_index(const Texture* t) {
-    for (size_t i = 0; i < tex_keys.size(); i++)
-        if (tex_keys[i] == t) return (uint32_t)i;
-    tex_keys.push_back(t);
+    auto it = tex_slot.find(t);
+    if (it != tex_slot.end()) return it->second;
+    const uint32_t idx = (uint32_t)textures.size();
+    tex_slot.emplace(t, idx);
     textures.push_back(gs_texture{});
-    uint32_t idx = (uint32_t)(textures.size() - 1);
     t->flatten(*this);
     return idx;
 }
 uint32_t Flattener::image_index(const ImageTexture* t) {
-    for (size_t i = 0; i < img_keys.size(); i++)
-        if (img_keys[i]->rgb8 == t->rgb8 && img_keys[i]->width == t->width && img_keys[i]->height == t->height)
-            return (uint32_t)i;
-    img_keys.push_back(t);
+    const auto key = std::make_tuple(t->rgb8, t->width, t->height);
+    auto it = img_slot.find(key);
+    if (it != img_slot.end()) return it->second;
     gs_image im{(uint32_t)t->width, (uint32_t)t->height, (uint64_t)texels8.size()};
     size_t n = (size_t)t->width * (size_t)t->height * 3;
     texels8.insert(texels8.end(), t->rgb8, t->rgb8 + n);
     images.push_back(im);
-    return (uint32_t)(images.size() - 1);
+    const uint32_t idx = (uint32_t)(images.size() - 1);
+    img_slot.emplace(key, idx);
+    return idx;
 }
 
-// A texture/material writes itself into the slot its *_index call reserved (the last
-// one whose key is `this`).
-static size_t slot_of(const std::vector<const Texture*>& keys, const Texture* t) {
-    for (size_t i = keys.size(); i-- > 0;)
-        if (keys[i] == t) return i;
-    throw std::logic_error("texture slot");
+// A texture/material writes itself into the slot its *_index call reserved.
+static size_t slot_of(const std::unordered_map<const Texture*, uint32_t>& slots, const Texture* t) {
+    auto it = slots.find(t);
+    if (it == slots.end()) throw std::logic_error("texture slot");
+    return it->second;
 }
-static size_t slot_of(const std::vector<const Material*>& keys, const Material* m) {
-    for (size_t i = keys.size(); i-- > 0;)
-        if (keys[i] == m) return i;
-    throw std::logic_error("material slot");
+static size_t slot_of(const std::unordered_map<const Material*, uint32_t>& slots, const Material* m) {
+    auto it = slots.find(m);
+    if (it == slots.end()) throw std::logic_error("material slot");
+    return it->second;
 }
 
 uint32_t SolidColorTexture::flatten(Flattener& f) const {
-    size_t s = slot_of(f.tex_keys, this);
+    size_t s = slot_of(f.tex_slot, this);
     gs_texture& t = f.textures[s];
     t.kind = GS_TEX_SOLID;
     albedo.store(t.color);
     return (uint32_t)s;
 }
 uint32_t CheckeredTexture::flatten(Flattener& f) const {
-    size_t s = slot_of(f.tex_keys, this);
+    size_t s = slot_of(f.tex_slot, this);
     uint32_t e = f.texture_index(even.get());
     uint32_t o = f.texture_index(odd.get());
     gs_texture& t = f.textures[s];
@@ -192,7 +192,7 @@ uint32_t CheckeredTexture::flatten(Flattener& f) const {
     return (uint32_t)s;
 }
 uint32_t ImageTexture::flatten(Flattener& f) const {
-    size_t s = slot_of(f.tex_keys, this);
+    size_t s = slot_of(f.tex_slot, this);
     if (width <= 0 || height <= 0 || !rgb8) throw std::invalid_argument("ImageTexture without texels");
     uint32_t im = f.image_index(this);
     gs_texture& t = f.textures[s];
@@ -237,7 +237,7 @@ void noise_permutation(uint32_t seed, uint8_t out[256]) {
 }
 
 uint32_t NoiseTexture::flatten(Flattener& f) const {
-    size_t s = slot_of(f.tex_keys, this);
+    size_t s = slot_of(f.tex_slot, this);
     if (f.noise_perm.empty()) {
         f.noise_perm.resize(256);
         noise_permutation(0, f.noise_perm.data());  // Perlin::DEFAULT_SEED
@@ -249,27 +249,27 @@ uint32_t NoiseTexture::flatten(Flattener& f) const {
 }
 
 uint32_t Lambertian::flatten(Flattener& f) const {
-    size_t s = slot_of(f.mat_keys, this);
+    size_t s = slot_of(f.mat_slot, this);
     uint32_t tex = f.texture_index(texture.get());
     f.materials[s].kind = GS_MAT_LAMBERTIAN;
     f.materials[s].texture = tex;
     return (uint32_t)s;
 }
 uint32_t Metal::flatten(Flattener& f) const {
-    size_t s = slot_of(f.mat_keys, this);
+    size_t s = slot_of(f.mat_slot, this);
     f.materials[s].kind = GS_MAT_METAL;
     albedo.store(f.materials[s].albedo);
     f.materials[s].param = fuzz;
     return (uint32_t)s;
 }
 uint32_t Dielectric::flatten(Flattener& f) const {
-    size_t s = slot_of(f.mat_keys, this);
+    size_t s = slot_of(f.mat_slot, this);
     f.materials[s].kind = GS_MAT_DIELECTRIC;
     f.materials[s].param = refraction_index;
     return (uint32_t)s;
 }
 uint32_t DiffuseLight::flatten(Flattener& f) const {
-    size_t s = slot_of(f.mat_keys, this);
+    size_t s = slot_of(f.mat_slot, this);
     uint32_t tex = f.texture_index(texture.get());
     f.materials[s].kind = GS_MAT_DIFFUSE_LIGHT;
     f.materials[s].texture = tex;
@@ -277,7 +277,7 @@ uint32_t DiffuseLight::flatten(Flattener& f) const {
 }
 
 uint32_t Isotropic::flatten(Flattener& f) const {
-    size_t s = slot_of(f.mat_keys, this);
+    size_t s = slot_of(f.mat_slot, this);
     uint32_t tex = f.texture_index(texture.get());
     f.materials[s].kind = GS_MAT_ISOTROPIC;
     f.materials[s].texture = tex;

@@ -18,10 +18,13 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <ostream>
 #include <stdexcept>
 #include <string>
+#include <tuple>
+#include <unordered_map>
 #include <vector>
 
 #include "../../../include/grayshift_gpu.h"
@@ -330,9 +333,11 @@ public:
     std::vector<gs_texture> textures;
     std::vector<gs_image> images;
     std::vector<uint8_t> texels8;
-    std::vector<const Material*> mat_keys;
-    std::vector<const Texture*> tex_keys;
-    std::vector<const ImageTexture*> img_keys;
+    // Identity -> slot (hash maps: a linear scan per lookup was O(n^2) in unique
+    // materials, minutes for a million-sphere world).
+    std::unordered_map<const Material*, uint32_t> mat_slot;
+    std::unordered_map<const Texture*, uint32_t> tex_slot;
+    std::map<std::tuple<const uint8_t*, int32_t, int32_t>, uint32_t> img_slot;  // same texels = one image
     uint32_t depth = 0, max_depth = 0;  // BVH node nesting while flattening
     bool inside_instance = false;
     bool inside_medium = false;  // flattening a ConstantMedium boundary

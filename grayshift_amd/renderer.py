@@ -44,6 +44,49 @@ def render_ppm(scene, seed=1):
     return buf.raw[:n.value], cnt.as_dict()
 
 
+def render_multi(scene, num_gpus=0, seed=1, tile=64, plan=True, rgb=True, rgb8=False, ppm=False, devices=None):
+    """camera.rs:105-114 (and with ppm=True the whole of :100-121) on `num_gpus` GPUs of
+    this node (0 = every visible one) through gs_render_multi: one scene per device,
+    tiles rendered concurrently, one RCCL gather to the first device.  Returns a dict
+    with the requested outputs ("rgb" [H,W,3] f32, "rgb8" [H,W,3] u8, "ppm" bytes), the
+    summed "counters" and the call's "stats"."""
+    host = HostScene(scene.spec)
+    try:
+        cam = camera(scene.camera)
+        H, W = cam.image_height, cam.image_width
+        res = {}
+        out = N.gs_multi_outputs()
+        if rgb:
+            res["rgb"] = np.zeros((H, W, 3), dtype=np.float32)
+            out.rgb = res["rgb"].ctypes.data
+        if rgb8:
+            res["rgb8"] = np.zeros((H, W, 3), dtype=np.uint8)
+            out.rgb8 = res["rgb8"].ctypes.data
+        n = C.c_int64(0)
+        if ppm:
+            cap = N.lib.gs_ppm_max_bytes(W, H)
+            buf = C.create_string_buffer(int(cap))
+            out.ppm_text = C.addressof(buf)
+            out.ppm_capacity = cap
+            out.ppm_len = C.pointer(n)
+        dev = None
+        if devices is not None:
+            dev = (C.c_int32 * len(devices))(*devices)
+            num_gpus = len(devices)
+        launch = N.gs_launch(num_gpus=num_gpus, tile_w=tile, tile_h=tile, plan=1 if plan else 0,
+                             devices=C.cast(dev, C.c_void_p) if dev is not None else None)
+        st = N.gs_stats()
+        N.check(N.lib.gs_render_multi(host.flat_ptr, C.byref(cam), C.byref(scene.settings), seed, C.byref(launch),
+                                      C.byref(out), C.byref(st)))
+        if ppm:
+            res["ppm"] = buf.raw[:n.value]
+        res["counters"] = {k: int(getattr(st.counters, k)) for k in N.COUNTER_NAMES}
+        res["stats"] = {k: getattr(st, k) for k, _ in N.gs_stats._fields_ if k not in ("counters", "pad")}
+        return res
+    finally:
+        host.close()
+
+
 def ppm_encode_async(d_rgb8, width, height, d_text, text_capacity, d_len, d_scratch, scratch_bytes, stream=0):
     """Format a device W*H*3 byte frame as the reference's PPM text on the device."""
     N.check(N.lib.gs_ppm_encode_async(C.c_void_p(d_rgb8), width, height, C.c_void_p(d_text), text_capacity,
@@ -89,9 +132,11 @@ class HostScene:
 class Renderer:
     """A scene resident in HBM of the current device, rendered tile-partitioned."""
 
-    def __init__(self, scene, rank=0, world_size=1, tile=64, tile_h=None, plan=False, plan_seed=1):
+    def __init__(self, scene, rank=0, world_size=1, tile=64, tile_h=None, plan=False, plan_seed=1, order=None):
         """plan: cost-balanced tile assignment (gs_plan_tiles: a 1-spp pilot of the whole
-        frame on this device, identical on every rank) instead of round-robin."""
+        frame on this device) instead of round-robin.  order: a plan computed elsewhere
+        (e.g. on rank 0 and broadcast: int32, slots_per_rank * world_size entries, see
+        gs_partition.d_tile_order), used as given."""
         self.scene = scene
         self.host = HostScene(scene.spec)
         self.cam = camera(scene.camera)
@@ -102,7 +147,9 @@ class Renderer:
         d = C.c_void_p()
         N.check(N.lib.gs_device_scene_create(self.host.flat_ptr, C.byref(d)))
         self.dev = d
-        if plan:
+        if order is not None:
+            self._use_order(np.ascontiguousarray(order, dtype=np.int32))
+        elif plan:
             self._plan(plan_seed)
         self.capacity = N.lib.gs_partition_capacity(C.byref(self.cam), C.byref(self.part))
         if self.capacity < 0:
@@ -116,13 +163,25 @@ class Renderer:
         order = np.zeros(slots.value * p.world_size, dtype=np.int32)
         N.check(N.lib.gs_plan_tiles(self.dev, C.byref(self.cam), seed, p.world_size, p.tile_w, p.tile_h,
                                     order.ctypes.data, order.size, C.byref(slots)))
+        self._use_order(order)
+
+    def _use_order(self, order):
+        p = self.part
+        if order.size % p.world_size:
+            raise ValueError("tile order of %d entries for %d ranks" % (order.size, p.world_size))
+        slots = order.size // p.world_size
+        ids = np.sort(order[order >= 0])
+        tx = (self.cam.image_width + p.tile_w - 1) // p.tile_w
+        ty = (self.cam.image_height + p.tile_h - 1) // p.tile_h
+        if not np.array_equal(ids, np.arange(tx * ty)):
+            raise ValueError("tile order must hold every tile exactly once")
         d = C.c_void_p()
         N.check(N.lib.gs_device_alloc(order.nbytes, C.byref(d)))
         self.d_order = d
         N.check(N.lib.gs_device_upload(d, order.ctypes.data, order.nbytes))
         self.order = order
         p.d_tile_order = d.value
-        p.slots_per_rank = slots.value
+        p.slots_per_rank = slots
 
     @property
     def width(self):

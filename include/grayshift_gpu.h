@@ -11,8 +11,10 @@
  *
  * Plain pointers and sizes only; no torch, no HIP types in the signatures (a stream
  * is passed as `void*`).  No exceptions cross the ABI: every entry point returns a
- * gs_status and leaves a message for gs_last_error().  Not reentrant on the same
- * gs_device_scene; reentrant on distinct scenes/devices.
+ * gs_status and leaves a message for gs_last_error().  Launches of one gs_device_scene
+ * may be issued from several host threads and on several streams: each launch takes
+ * its own parameter / work-queue / chunk-sum slot from a small ring (a slot is reused
+ * only after its previous launch has finished, by a stream wait on that launch's event).
  */
 #ifndef GRAYSHIFT_GPU_H
 #define GRAYSHIFT_GPU_H
@@ -25,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 3
+#define GS_ABI_VERSION 4
 
 typedef int32_t gs_status;
 enum {
@@ -222,6 +224,10 @@ int32_t gs_version(void);
  * so only the association of the f64 colour sum differs from the sequential loop. */
 gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf_batch, int32_t sample_chunk);
 
+/* Test hook: the auto sample-chunk rule's budget for chunk sums (default 4 GiB; 0
+ * restores it).  A smaller budget makes renders take the chunk-doubling branch. */
+gs_status gs_debug_set_partial_budget(uint64_t bytes);
+
 /* Upload a flattened scene to the current HIP device. */
 gs_status gs_device_scene_create(const gs_flat_scene* scene, gs_device_scene** out);
 gs_status gs_device_scene_destroy(gs_device_scene* scene);
@@ -254,7 +260,7 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* scene, const gs_camera
                                    gs_counters* d_counters, void* stream);
 
 /* Diagnostic variant: also writes, per packed pixel, the number of BVH node visits
- * its samples made (d_item_visits: capacity u32, nullable). */
+ * its samples made (d_item_visits: capacity u32, nullable; zeroed by the call). */
 gs_status gs_render_tiles_debug_async(const gs_device_scene* scene, const gs_camera* cam,
                                       const gs_sample_settings* ss, uint64_t seed,
                                       const gs_partition* part, float* d_packed_rgb,
@@ -308,6 +314,51 @@ gs_status gs_plan_tiles(const gs_device_scene* scene, const gs_camera* cam, uint
 /* Unpack for any partition (incl. d_tile_order): elem_bytes 12 (f32 rgb) or 3 (rgb8). */
 gs_status gs_unpack_tiles_part_async(const gs_camera* cam, const gs_partition* part, int64_t capacity,
                                      const void* d_gathered, void* d_frame, int32_t elem_bytes, void* stream);
+
+/* ---- The N-GPU render behind one call (ABI 4) ----
+ * The whole pixel loop of camera.rs:105-114 on the GPUs of one node, from one host
+ * thread: the scene is uploaded to every device, the frame is cut into tile_w x tile_h
+ * tiles (plan = 1: cost-balanced, gs_plan_tiles on the first device; 0: round-robin),
+ * each device renders its tiles on its own stream, ONE grouped RCCL gather (ncclGather
+ * over xGMI, communicator from ncclCommInitAll, one rank per device) brings the packed
+ * tiles to the first device, which unpacks them (and formats the PPM text when asked).
+ * The frame equals gs_render's for every device count (per-pixel RNG streams).
+ * Synchronous; RCCL is loaded at the first call (GS_ERR_UNSUPPORTED without it). */
+typedef struct gs_launch {
+    int32_t num_gpus;       /* devices used; 0 = every visible device */
+    int32_t tile_w, tile_h; /* 0 = 64 (tile_h 0 = tile_w) */
+    int32_t plan;           /* 1: cost-balanced tiles, 0: round-robin */
+    const int32_t* devices; /* nullable: num_gpus distinct HIP device ids (default 0..num_gpus-1) */
+} gs_launch;
+
+/* Host outputs of gs_render_multi; any subset, at least one. */
+typedef struct gs_multi_outputs {
+    float* rgb;           /* W*H*3 f32, linear colour (camera.rs:167), nullable */
+    uint8_t* rgb8;        /* W*H*3 write_color bytes of the f64 colour, nullable */
+    char* ppm_text;       /* the PPM file Camera::render writes (camera.rs:101-118), nullable */
+    int64_t ppm_capacity; /* >= gs_ppm_max_bytes(W, H) when ppm_text is set */
+    int64_t* ppm_len;     /* receives the text length when ppm_text is set */
+} gs_multi_outputs;
+
+/* What one gs_render_multi call did (SURVEY.md §5 metrics). */
+typedef struct gs_stats {
+    gs_counters counters;       /* summed over devices */
+    double setup_ms;            /* host: scene uploads + tile plan */
+    double total_ms;            /* host: the whole call */
+    double render_ms_max;       /* slowest device's render launch (HIP events) */
+    double render_ms_min;       /* fastest device's */
+    double gather_ms;           /* first device: RCCL gather + unpack (HIP events) */
+    uint64_t algorithmic_bytes; /* SURVEY.md §8d bytes of every launch (cache-served, not HBM) */
+    uint64_t gathered_bytes;    /* bytes the gather delivered to the first device */
+    int32_t num_gpus;
+    int32_t pad;
+} gs_stats;
+
+gs_status gs_render_multi(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss,
+                          uint64_t seed, const gs_launch* launch, const gs_multi_outputs* out, gs_stats* stats);
+
+/* Path of the RCCL library gs_render_multi uses (loaded on this call), or NULL. */
+const char* gs_rccl_library(void);
 
 /* Device memory helpers for callers without their own allocator (ctypes, FFI). */
 gs_status gs_device_alloc(int64_t bytes, void** d_out);

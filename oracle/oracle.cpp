@@ -30,6 +30,7 @@
 #include <cfloat>
 #include <climits>
 #include <atomic>
+#include <chrono>
 #include <memory>
 #include <thread>
 #include <vector>
@@ -1094,13 +1095,15 @@ int32_t oracle_color_byte(double c);
  * (n_pixels*3 f32, in subset order, or the full W*H*3 frame), and, when out_rgb8 is
  * not NULL, write_color's bytes of the f64 colour in the same order.
  * Returns 0 on success, -1 on error (message in oracle_last_error). */
-int oracle_render(const gs_scene_spec* spec, const gs_camera_spec* cam, const gs_sample_settings* ss,
-                  uint64_t seed, int32_t n_threads, const int32_t* subset, int64_t n_subset,
-                  float* out_rgb, gs_counters* counters, uint8_t* out_rgb8) {
+int oracle_render_timed(const gs_scene_spec* spec, const gs_camera_spec* cam, const gs_sample_settings* ss,
+                        uint64_t seed, int32_t n_threads, const int32_t* subset, int64_t n_subset,
+                        float* out_rgb, gs_counters* counters, uint8_t* out_rgb8, double* render_seconds) {
     try {
         World w;
         build_world(*spec, w);
         Camera camera(*cam, *ss, spec->background, seed);
+        /* render time only: the pixel loop (camera.rs:105-114), not the world / BVH build */
+        const auto t0 = std::chrono::steady_clock::now();
         int64_t n = subset ? n_subset : (int64_t)camera.image_width * camera.image_height;
         if (n_threads <= 0) n_threads = (int32_t)std::max(1u, std::thread::hardware_concurrency());
         std::atomic<int64_t> next(0);
@@ -1135,6 +1138,8 @@ int oracle_render(const gs_scene_spec* spec, const gs_camera_spec* cam, const gs
             });
         }
         for (auto& x : th) x.join();
+        if (render_seconds)
+            *render_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         for (auto& e : errs) if (!e.empty()) throw std::runtime_error(e);
         if (counters) {
             std::memset(counters, 0, sizeof(*counters));
@@ -1145,6 +1150,13 @@ int oracle_render(const gs_scene_spec* spec, const gs_camera_spec* cam, const gs
         tl_err = ex.what();
         return -1;
     }
+}
+
+int oracle_render(const gs_scene_spec* spec, const gs_camera_spec* cam, const gs_sample_settings* ss,
+                  uint64_t seed, int32_t n_threads, const int32_t* subset, int64_t n_subset,
+                  float* out_rgb, gs_counters* counters, uint8_t* out_rgb8) {
+    return oracle_render_timed(spec, cam, ss, seed, n_threads, subset, n_subset, out_rgb, counters, out_rgb8,
+                               nullptr);
 }
 
 /* Camera::new derived fields, for KATs: image_height, center, starting_pixel_pos,

@@ -28,6 +28,8 @@ def lib():
         L.oracle_render.argtypes = [C.POINTER(N.gs_scene_spec), C.POINTER(N.gs_camera_spec),
                                     C.POINTER(N.gs_sample_settings), C.c_uint64, C.c_int32, P, C.c_int64, P,
                                     C.POINTER(N.gs_counters), P]
+        L.oracle_render_timed.restype = C.c_int
+        L.oracle_render_timed.argtypes = L.oracle_render.argtypes + [C.POINTER(C.c_double)]
         L.oracle_noise_perm.argtypes = [C.c_uint32, P]
         L.oracle_perlin3.restype = C.c_double
         L.oracle_perlin3.argtypes = [P]
@@ -63,9 +65,10 @@ def _d(a):
     return a, a.ctypes.data
 
 
-def render(scene, seed=1, threads=0, subset=None, bytes_out=False):
+def render(scene, seed=1, threads=0, subset=None, bytes_out=False, timing=None):
     """Render `scene` (scenes.Scene) on the CPU.  Returns (rgb f32 [n,3] or [H,W,3], counters dict),
-    plus write_color's bytes of the f64 colour (u8, same shape) when bytes_out."""
+    plus write_color's bytes of the f64 colour (u8, same shape) when bytes_out.
+    timing: a dict that receives "render_s", the pixel loop's wall time (world/BVH build excluded)."""
     from grayshift_amd import _native as N
     L = lib()
     if not threads:  # the GPU box's CPU share is 16 cores; nproc reports the whole machine
@@ -79,8 +82,12 @@ def render(scene, seed=1, threads=0, subset=None, bytes_out=False):
         out = np.zeros((scene.height, scene.width, 3), dtype=np.float32)
         sub_ptr, n_sub = None, 0
     b8 = np.zeros(out.shape, dtype=np.uint8) if bytes_out else None
-    r = L.oracle_render(scene.spec.ptr(), C.byref(scene.camera), C.byref(scene.settings), seed, threads,
-                        sub_ptr, n_sub, out.ctypes.data, C.byref(cnt), b8.ctypes.data if bytes_out else None)
+    secs = C.c_double(0.0)
+    r = L.oracle_render_timed(scene.spec.ptr(), C.byref(scene.camera), C.byref(scene.settings), seed, threads,
+                              sub_ptr, n_sub, out.ctypes.data, C.byref(cnt), b8.ctypes.data if bytes_out else None,
+                              C.byref(secs))
+    if timing is not None:
+        timing["render_s"] = secs.value
     if r != 0:
         raise RuntimeError("oracle: " + L.oracle_last_error().decode())
     if bytes_out:

@@ -297,3 +297,26 @@ def test_full_size_frames(name, spp):
     if name == "C1":  # small enough to check every pixel
         ref, rc = oracle.render(sc, seed=1)
         assert maxdiff(out, ref) < TOL and counters_match(c, rc)
+
+
+# ------------------------------------- C3 / C5 at their stated spp (auto chunks)
+@pytest.mark.parametrize("name,width,cpp", [("C3", 64, None), ("C5", 64, None), ("C5", 64, 16), ("C5", 48, 8)])
+def test_stated_spp_configs_vs_oracle(name, width, cpp):
+    """C3 at its full 1024 spp and C5 at its full 4096 spp (reduced width), rendered
+    through the auto sample-chunk rule (render.hip: 16-sample chunks, or batch/64, then
+    doubled while the chunk sums exceed the budget).  C3 at 1024 spp: 64 chunks of 16
+    per pixel.  C5 at 3840x2160 takes the doubling branch (4096 spp: 256-sample chunks,
+    16 per pixel); a test budget of capacity x cpp x 24 bytes makes this small frame
+    take the same branch (cpp = 16: 256-sample chunks; cpp = 8: 512)."""
+    sc = scenes.config(name, width=width)
+    cam = g.camera(sc.camera)
+    cap = N.lib.gs_partition_capacity(C.byref(cam), C.byref(N.gs_partition(0, 1, 64, 64)))
+    if cpp:
+        N.check(N.lib.gs_debug_set_partial_budget(cap * cpp * 24))
+    try:
+        out, gc = g.render(sc, seed=17)
+    finally:
+        N.check(N.lib.gs_debug_set_partial_budget(0))
+    ref, rc = oracle.render(sc, seed=17)
+    assert gc["paths"] == sc.width * sc.height * sc.settings.batch_size
+    assert maxdiff(out, ref) < TOL and counters_match(gc, rc)

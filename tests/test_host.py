@@ -39,7 +39,7 @@ def test_every_declared_symbol_is_exported(built):
 
 
 def test_version_and_error_channel():
-    assert N.lib.gs_version() == N.GS_ABI_VERSION == 3
+    assert N.lib.gs_version() == N.GS_ABI_VERSION == 4
     assert N.lib.gs_set_tuning(0, 0, 0, -1) == N.GS_ERR_ARG
     assert b"tuning" in N.lib.gs_last_error()
     assert N.lib.gs_set_tuning(60, 0, 0, -1) == N.GS_OK
@@ -49,7 +49,8 @@ def test_version_and_error_channel():
 
 @pytest.mark.parametrize("name", ["gs_object", "gs_material_spec", "gs_texture_spec", "gs_image_spec",
                                   "gs_background_spec", "gs_scene_spec", "gs_camera_spec", "gs_sample_settings",
-                                  "gs_counters", "gs_camera", "gs_partition", "gs_background", "gs_flat_scene"])
+                                  "gs_counters", "gs_camera", "gs_partition", "gs_background", "gs_flat_scene",
+                                  "gs_render_outputs", "gs_launch", "gs_multi_outputs", "gs_stats"])
 def test_struct_layouts_match(name):
     assert N.lib.gs_host_struct_size(name.encode()) == C.sizeof(getattr(N, name))
 
@@ -308,7 +309,8 @@ def test_rust_binding_declares_every_gpu_entry_point():
     assert "pub const GS_ABI_VERSION: i32 = %d;" % N.GS_ABI_VERSION in _rust()
 
 
-@pytest.mark.parametrize("name", ["gs_counters", "gs_flat_scene", "gs_camera", "gs_render_outputs", "gs_medium"])
+@pytest.mark.parametrize("name", ["gs_counters", "gs_flat_scene", "gs_camera", "gs_render_outputs", "gs_medium",
+                                  "gs_launch", "gs_multi_outputs", "gs_stats"])
 def test_rust_struct_fields_follow_the_header(name):
     """Field names in declaration order (arrays flattened by name) match the C struct."""
     hdrs = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("grayshift_gpu.h", "grayshift_scene.h"))
@@ -357,10 +359,97 @@ def test_plan_and_device_helpers_reject_bad_arguments_before_the_device():
 
 
 def test_library_shares_torchs_hip_runtime():
-    """_native loads torch before libgrayshift.so so one HIP runtime serves both (torch's
-    bundled libamdhip64.so.7 and /opt/rocm's share a soname; whichever loads first wins)."""
-    import sys
-    assert "torch" in sys.modules
+    """_native loads torch's bundled libamdhip64.so.7 (by path, without importing torch)
+    before libgrayshift.so, so one HIP runtime serves both (torch's and /opt/rocm's share
+    a soname; whichever loads first wins)."""
+    pytest.importorskip("torch")
+    import grayshift_amd  # noqa: F401  (the library is loaded at import)
     maps = open("/proc/self/maps").read()
     hips = {line.split()[-1] for line in maps.splitlines() if "libamdhip64" in line}
     assert len(hips) == 1, hips
+    assert "/torch/lib/" in next(iter(hips)), hips
+
+
+# ------------------------------------------------------- flattener scalability
+def _million_sphere_spec(n_side=1000):
+    """A bouncing_spheres-like world of n_side^2 small spheres, every one with its own
+    Lambertian over its own solid texture (unique materials, as main.rs:85-110 makes),
+    plus the checkered ground; built directly as spec arrays (numpy), not by the Python
+    scene builder."""
+    n = n_side * n_side
+    rng = np.random.default_rng(7)
+    objs = np.zeros(n + 1, dtype=np.dtype(N.gs_object))
+    objs["kind"] = N.GS_OBJ_SPHERE
+    a, b = np.meshgrid(np.arange(n_side) - n_side // 2, np.arange(n_side) - n_side // 2, indexing="ij")
+    objs["p"][:n, 0] = a.ravel() + 0.9 * rng.random(n)
+    objs["p"][:n, 1] = 0.2
+    objs["p"][:n, 2] = b.ravel() + 0.9 * rng.random(n)
+    objs["p"][:n, 3] = 0.2
+    objs["material"][:n] = np.arange(n)
+    objs["p"][n, :4] = (0.0, -1000.0, 0.0, 1000.0)  # ground
+    objs["material"][n] = n
+    mats = np.zeros(n + 1, dtype=np.dtype(N.gs_material_spec))
+    mats["kind"] = N.GS_MAT_LAMBERTIAN
+    mats["texture"] = np.arange(n + 1)
+    mats["texture"][n] = n + 2  # ground: the checker over two solids
+    texs = np.zeros(n + 3, dtype=np.dtype(N.gs_texture_spec))
+    texs["kind"] = N.GS_TEX_SOLID
+    texs["p"][:n] = rng.random((n, 3))
+    texs["kind"][n + 2], texs["a"][n + 2], texs["b"][n + 2] = N.GS_TEX_CHECKERED, n, n + 1
+    texs["p"][n + 2, 0] = 0.32
+    world = np.arange(n + 1, dtype=np.int32)
+    s = N.gs_scene_spec()
+    s.objects, s.n_objects = C.cast(objs.ctypes.data, C.POINTER(N.gs_object)), n + 1
+    s.world, s.n_world = C.cast(world.ctypes.data, C.POINTER(C.c_int32)), n + 1
+    s.materials, s.n_materials = C.cast(mats.ctypes.data, C.POINTER(N.gs_material_spec)), n + 1
+    s.textures, s.n_textures = C.cast(texs.ctypes.data, C.POINTER(N.gs_texture_spec)), n + 3
+    s.background = N.gs_background_spec(kind=N.GS_BG_SOLID)
+    return s, (objs, mats, texs, world)
+
+
+def test_million_sphere_world_flattens_in_seconds():
+    """World + BVHNode::from_list + flatten of ~1M spheres with ~1M unique materials: the
+    flattener's identity lookups are hash maps (a linear scan per lookup took hours)."""
+    import time
+    spec, keep = _million_sphere_spec()
+    t0 = time.perf_counter()
+    h = C.c_void_p()
+    N.check(N.lib.gs_host_scene_from_spec(C.byref(spec), C.byref(h)))
+    dt = time.perf_counter() - t0
+    try:
+        f = N.gs_flat_scene.from_address(N.lib.gs_host_scene_flat(h))
+        assert f.n_spheres == 1000 * 1000 + 1
+        assert f.n_materials == 1000 * 1000 + 1 and f.n_textures == 1000 * 1000 + 3
+        assert f.n_nodes >= f.n_spheres // 2
+    finally:
+        N.lib.gs_host_scene_destroy(h)
+    assert dt < 5.0, "flatten took %.1f s" % dt
+
+
+# ------------------------------------------- Rust flattener (INTEGRATION.md §2)
+def test_rust_scene_builder_mirrors_the_cpp_flattener():
+    rs = _rust()
+    assert "pub struct SceneBuilder" in rs and "pub struct FlatScene" in rs
+    impl = rs[rs.index("impl SceneBuilder"):]
+    methods = set(re.findall(r"pub fn ([a-z_]+)\s*\(", impl))
+    # one builder method per flattened record kind, the identity lookups, and finish
+    assert {"node", "sphere", "moving_sphere", "quad", "triangle", "list", "instance", "medium", "material_index",
+            "texture_index", "image_index", "finish"} <= methods
+    # identity lookups are hash maps (O(1)), as the C++ Flattener's
+    assert "HashMap" in rs and "mat_slot" in rs and "tex_slot" in rs
+    # SceneBuilder fills every array of gs_flat_scene
+    fin = impl[impl.index("pub fn finish"):]
+    body = re.search(r"typedef struct gs_flat_scene \{(.*?)\} gs_flat_scene;",
+                     re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "grayshift_gpu.h")).read(), flags=re.S),
+                     re.S).group(1)
+    for field in re.findall(r"([a-z_0-9]+)\s*;", body):
+        assert field + ":" in fin or field + "," in fin, field
+
+
+def test_integration_example_uses_the_binding():
+    """The Rust example in INTEGRATION.md calls only what bindings/grayshift_gpu.rs defines."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    rs = _rust()
+    for name in re.findall(r"gs::([A-Za-z_]+)", doc):
+        assert re.search(r"pub (?:fn|struct|const) %s\b" % name, rs), name
+    assert "b.finish(" in doc and "pub fn finish" in rs

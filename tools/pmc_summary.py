@@ -1,6 +1,9 @@
 """Fold tools/pmc.sh's per-pass rocprofv3 CSVs into one JSON per kernel launch.
 
-    python tools/pmc_summary.py gpurun_out profiles/pmc_C4_latest.json [--kernel gs_render_kernel]
+    python tools/pmc_summary.py gpurun_out profiles/pmc [--config C4] [--kernel gs_render_kernel]
+
+Writes <out_dir>/<config>_<code-object hash>.json: bench.py reads the summary of the very
+code object it times (grayshift_amd/codeobj.py hashes libgrayshift.so's gfx950 code).
 
 Counter values are summed over the kernel's dispatches and divided by their number
 (per-launch figures).  HBM bytes follow MI355X_MICROARCH.md's gfx950 correction:
@@ -21,8 +24,15 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--kernel", default="gs_render_kernel")
     ap.add_argument("--config", default="C4")
-    ap.add_argument("--round", type=int, default=1)
+    ap.add_argument("--round", type=int, default=2)
+    ap.add_argument("--lib", default=None, help="the library profiled (default: the in-tree libgrayshift.so)")
     a = ap.parse_args()
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from grayshift_amd.codeobj import code_object_hash
+    lib = a.lib or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "grayshift_amd",
+                                "libgrayshift.so")
+    h = code_object_hash(lib)
     vals = defaultdict(float)
     dispatches = defaultdict(set)
     dur = []
@@ -43,7 +53,7 @@ def main():
     c = {k: vals[k] / len(dispatches[k]) for k in sorted(vals)}
     fetch, write = c.get("FETCH_SIZE", 0.0) * 1024, c.get("WRITE_SIZE", 0.0) * 1024
     out = {
-        "config": a.config, "kernel": a.kernel, "round": a.round,
+        "config": a.config, "kernel": a.kernel, "round": a.round, "code_object": h,
         "source": "tools/pmc.sh on MI355X: rocprofv3 --kernel-trace --pmc, one pass per counter group, "
                   "one frame per pass; folded by tools/pmc_summary.py",
         "kernel_duration_ms_profiled": sum(dur) / len(dur) if dur else None,
@@ -59,8 +69,18 @@ def main():
     if "SQ_WAVE_CYCLES" in c:
         out["wait_any_frac"] = c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
         out["active_inst_frac"] = c.get("SQ_ACTIVE_INST_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
-    with open(a.out, "w") as f:
+    if "SQ_INSTS_VALU" in c and "GRBM_GUI_ACTIVE" in c:
+        cyc = c["GRBM_GUI_ACTIVE"] / 8.0  # per-XCD cycles (rocprofv3 sums the 8 XCDs)
+        out["valu_issue_frac"] = c["SQ_INSTS_VALU"] * 4 / (1024 * cyc)
+        if "SQ_ACTIVE_INST_VALU" in c:
+            out["valu_active_frac"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * cyc)
+        if "SQ_INSTS_SALU" in c:
+            out["salu_issue_frac"] = c["SQ_INSTS_SALU"] / (1024 * cyc)
+    os.makedirs(a.out, exist_ok=True)
+    path = os.path.join(a.out, "%s_%s.json" % (a.config, h))
+    with open(path, "w") as f:
         json.dump(out, f, indent=1)
+    print(path)
     print(json.dumps({k: out[k] for k in ("hbm_bytes_per_launch", "kernel_duration_ms_profiled")}))
 
 
