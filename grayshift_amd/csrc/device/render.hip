@@ -138,13 +138,16 @@ struct KParams {
 
 // Hot kernel arguments: what the traversal loop reads every step.
 struct KArgs {
-    const DNode* nodes;  // the threaded top-level records
+    const TNode* tnodes;   // the threaded top-level tree: node records (f32 box, links)
+    const TLeaf* tleaves;  // its leaf records
+    const TBox* tboxes;    // the f64 box of each node record (undecided / non-cert rays)
     const KParams* P;
     uint32_t root;
     int32_t shade_batch;
     int32_t leaf_batch;  // >= 1: tracing lanes at a leaf before a wave runs a leaf pass
-    int32_t fast_boxes;  // every node coordinate |x| < 1e300: rays may take box_hit_fast
-    uint32_t lds_top;    // threaded records [0, lds_top) are mirrored in each block's LDS
+    int32_t cert_boxes;  // every node coordinate |x| <= 1e15: cert rays may take box_cert
+    uint32_t lds_nodes;  // node records [0, lds_nodes) are mirrored in each block's LDS,
+    uint32_t lds_leaves; // then leaf records [0, lds_leaves)
 };
 
 enum { S_NEED = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };
@@ -174,20 +177,9 @@ __host__ __device__ inline uint32_t device_ref(uint32_t abi_ref) {
 #define THR_END 0x7FFFFFFFu
 #define THR_LEAF 0x80000000u
 
-__device__ __forceinline__ void load_leaf_rec(const DNode* p, double& cx, double& cy, double& cz, double& r,
-                                              uint32_t& next, uint32_t& ref) {
-    const uint4* q = reinterpret_cast<const uint4*>(p);
-    const uint4 a = q[0], b = q[1];
-    const uint2 d = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(p) + 48);
-    cx = __hiloint2double((int)a.y, (int)a.x);
-    cy = __hiloint2double((int)a.w, (int)a.z);
-    cz = __hiloint2double((int)b.y, (int)b.x);
-    r = __hiloint2double((int)b.w, (int)b.z);
-    next = d.x;
-    ref = d.y;
-}
-
-// The same two loads from the LDS mirror.  Address-space-qualified pointers keep them
+// Node and leaf records live in two arrays (32-B TNode, 48-B TLeaf: geometry.hpp); a link
+// is a node index, THR_LEAF | a leaf index, or THR_END.  Each block mirrors the most-tested
+// prefix of both arrays in LDS.  Address-space-qualified pointers keep the mirror reads
 // ds_read instructions: a select between an LDS and a global pointer would compile to
 // flat loads, which measured 34% slower on the whole kernel.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -195,28 +187,46 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
 typedef __attribute__((address_space(3))) const u32x2 lds_u32x2;
 __device__ __forceinline__ double lo_hi(unsigned int lo, unsigned int hi) { return __hiloint2double((int)hi, (int)lo); }
-__device__ __forceinline__ DNode load_node56_lds(const uint8_t* p) {
-    lds_u32x4* q = (lds_u32x4*)(p);
-    const u32x4 a = q[0], b = q[1], c = q[2];
-    const u32x2 d = *(lds_u32x2*)(p + 48);
-    DNode n;
-    n.mnx = lo_hi(a.x, a.y);
-    n.mny = lo_hi(a.z, a.w);
-    n.mnz = lo_hi(b.x, b.y);
-    n.mxx = lo_hi(b.z, b.w);
-    n.mxy = lo_hi(c.x, c.y);
-    n.mxz = lo_hi(c.z, c.w);
-    n.left = d.x;
-    n.right = d.y;
-    n.pad0 = 0;
-    n.pad1 = 0;
-    return n;
+
+// A node record (2 x 16 B): a = (mnx, mny, mnz, mxx), b = (mxy, mxz, hit, miss).
+// (Offsets are u32: indices < 2^26, so i * 48 < 2^32 — one SGPR base + a 32-bit VGPR offset.)
+__device__ __forceinline__ void load_tnode(const uint8_t* s_nodes, const TNode* g, uint32_t i, uint32_t lds_n,
+                                           u32x4& a, u32x4& b) {
+    if (i < lds_n) {
+        lds_u32x4* q = (lds_u32x4*)(s_nodes + (i << 5));
+        a = q[0];
+        b = q[1];
+    } else {
+        const u32x4* q = reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(g) + (i << 5));
+        a = q[0];
+        b = q[1];
+    }
 }
-__device__ __forceinline__ void load_leaf_rec_lds(const uint8_t* p, double& cx, double& cy, double& cz, double& r,
-                                                  uint32_t& next, uint32_t& ref) {
-    lds_u32x4* q = (lds_u32x4*)(p);
-    const u32x4 a = q[0], b = q[1];
-    const u32x2 d = *(lds_u32x2*)(p + 48);
+// 1/d for the f64 slab test on the rare paths.  The asm barrier keeps the compiler from
+// hoisting these divisions out of the traversal loop (d is loop-invariant) into six
+// registers live across the whole loop: recomputed where needed, they cost nothing in
+// the common path.
+__device__ __forceinline__ d3 inv_of(d3 d) {
+    asm volatile("" : "+v"(d.x), "+v"(d.y), "+v"(d.z));
+    return mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+}
+// A leaf record: the sphere's centre and radius, its next link and its ABI ref.
+__device__ __forceinline__ void load_tleaf(const uint8_t* s_leaves, const TLeaf* g, uint32_t i, uint32_t lds_l,
+                                           double& cx, double& cy, double& cz, double& r, uint32_t& next,
+                                           uint32_t& ref) {
+    u32x4 a, b;
+    u32x2 d;
+    if (i < lds_l) {
+        const uint8_t* p = s_leaves + i * 48u;
+        a = ((lds_u32x4*)p)[0];
+        b = ((lds_u32x4*)p)[1];
+        d = *(lds_u32x2*)(p + 32);
+    } else {
+        const char* p = reinterpret_cast<const char*>(g) + i * 48u;
+        a = reinterpret_cast<const u32x4*>(p)[0];
+        b = reinterpret_cast<const u32x4*>(p)[1];
+        d = *reinterpret_cast<const u32x2*>(p + 32);
+    }
     cx = lo_hi(a.x, a.y);
     cy = lo_hi(a.z, a.w);
     cz = lo_hi(b.x, b.y);
@@ -667,7 +677,8 @@ __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull <<
 // Per-lane pixel state lives in LDS ([field][lane], conflict-free), touched once per
 // path; the mirror of the tree's top records follows it.
 enum { L_CSR = 0, L_CSG, L_CSB, L_LSUM, L_LSQ, L_SCOUNT, L_ND };
-enum { L_ITEM = 0, L_PIX, L_BLEFT, L_NI };
+enum { L_ITEM = 0, L_PIX, L_BLEFT, L_SAMPLE, L_DEPTH, L_HINST, L_NI };  // (sample, depth, hit
+// instance: per-path state touched once per bounce, kept out of the traversal loop's VGPRs)
 
 __host__ __device__ constexpr size_t lane_lds_bytes() { return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4); }
 
@@ -682,13 +693,17 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     double* s_d = (double*)smem;                                  // [L_ND][GS_BLOCK]
     uint32_t* s_i = (uint32_t*)(smem + L_ND * 8 * GS_BLOCK);      // [L_NI][GS_BLOCK]
     // The records a ray most likely tests (placed first by the host) are mirrored in LDS;
-    // a lane whose record index is below lds_top reads it from there (ds_read), the rest
-    // from global memory.
-    uint8_t* s_top = smem + lane_lds_bytes();
+    // a lane whose node / leaf index is below lds_nodes / lds_leaves reads it from there
+    // (ds_read), the rest from global memory.
+    uint8_t* s_nodes = smem + lane_lds_bytes();
+    uint8_t* s_leaves = s_nodes + (size_t)A.lds_nodes * sizeof(TNode);
     {
-        const uint4* src = reinterpret_cast<const uint4*>(A.nodes);
-        uint4* dst = reinterpret_cast<uint4*>(s_top);
-        for (uint32_t k = threadIdx.x; k < A.lds_top * 4u; k += GS_BLOCK) dst[k] = src[k];
+        const uint4* src = reinterpret_cast<const uint4*>(A.tnodes);
+        uint4* dst = reinterpret_cast<uint4*>(s_nodes);
+        for (uint32_t k = threadIdx.x; k < A.lds_nodes * 2u; k += GS_BLOCK) dst[k] = src[k];
+        src = reinterpret_cast<const uint4*>(A.tleaves);
+        dst = reinterpret_cast<uint4*>(s_leaves);
+        for (uint32_t k = threadIdx.x; k < A.lds_leaves * 3u; k += GS_BLOCK) dst[k] = src[k];
     }
     if (threadIdx.x < C_N) s_cnt[threadIdx.x] = 0;
     __syncthreads();
@@ -706,30 +721,32 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     bool qdone = false;
     uint32_t res_base = 0, res_cnt = 0;  // the wave's reserve of claimed items (wave-uniform)
     // path state (registers)
-    uint32_t sample = 0, depth = 0;
     uint64_t rng = 0;
     double Tr = 1, Tg = 1, Tb = 1;
     Ray ray;
     ray.o = mk(0, 0, 0);
     ray.d = mk(0, 0, 0);
     ray.time = 0;
-    d3 inv = mk(0, 0, 0);
+    RayCert rc{};  // the ray in the certified f32 slab test's terms (geometry.hpp)
     // traversal state
-    uint32_t cur = THR_END, hit_ref = GS_REF_NONE, hit_inst = GS_REF_NONE;
+    uint32_t cur = THR_END, hit_ref = GS_REF_NONE;
     double closest = 0.0;
-    bool fast = false;  // this ray's slab times can never be NaN (geometry.hpp box_hit_fast)
+    float closest32 = 0.0f;  // f32(closest)
+    const float tmin32 = 0.001f;  // f32(tmin)
+    bool fast = false;  // a cert ray: nodes take box_cert (geometry.hpp)
     // hot counters kept in registers, flushed per pixel
     uint32_t c_nodes = 0, c_sph = 0;  // (per lane: one VALU add beat a 64-bit SALU wave count)
 
     auto begin_ray = [&]() {
-        inv = mk(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
-#ifndef GS_NO_FAST_SLAB
-        fast = A.fast_boxes && fast_slab_ray(ray.o, inv);
-#endif
+        // AABB::hit's `1.0 / ray.direction[axis]` (AABB.rs:64), hoisted per ray (same value)
+        const d3 inv = mk(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
+        fast = A.cert_boxes && cert_ray_ok(ray.o, inv);
+        rc = make_cert(ray.o, inv);
         cur = A.root;  // the root record's link (THR_*)
         closest = 1.7976931348623157e308;  // f64::MAX (camera.rs:177)
+        closest32 = __builtin_inff();
         hit_ref = GS_REF_NONE;
-        hit_inst = GS_REF_NONE;
+        LI(L_HINST) = GS_REF_NONE;
         atomicAdd(&s_cnt[C_RAYS], 1ull);
     };
 
@@ -743,7 +760,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             LD(L_LSUM) += lum;
             LD(L_LSQ) += lum * lum;
         }
-        sample++;
+        LI(L_SAMPLE) += 1u;
         LI(L_BLEFT) -= 1u;
     };
 
@@ -810,7 +827,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             // Camera::get_ray (camera.rs:204-221) on the seeded stream of this sample
             const uint32_t pix = LI(L_PIX);
             const uint32_t pi = pix % (uint32_t)cam.image_width, pj = pix / (uint32_t)cam.image_width;
-            rng = stream_seed(P->seed, pix, sample);
+            rng = stream_seed(P->seed, pix, LI(L_SAMPLE));
             atomicAdd(&s_cnt[C_PATHS], 1ull);
             double offx = wy_f64(rng) - 0.5;
             double offy = wy_f64(rng) - 0.5;
@@ -834,8 +851,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             ray.d = sub(ps, org);
             ray.time = wy_f64(rng);
             Tr = Tg = Tb = 1.0;
-            depth = cam.max_depth;
-            if (depth > 0) {
+            LI(L_DEPTH) = cam.max_depth;
+            if (cam.max_depth > 0) {
                 begin_ray();
                 st = S_TRACE;
                 return;
@@ -929,13 +946,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         LD(L_SCOUNT) = 0.0 + (double)P->ss.batch_size;
                         if (P->chunk) {
                             LI(L_ITEM) = item * cpp + ck;
-                            sample = ck * P->chunk;
-                            LI(L_BLEFT) = min(P->chunk, P->ss.batch_size - sample);
+                            LI(L_SAMPLE) = ck * P->chunk;
+                            LI(L_BLEFT) = min(P->chunk, P->ss.batch_size - ck * P->chunk);
                             if (ck == 0) atomicAdd(&s_cnt[C_PIX], 1ull);
                         } else {
                             LI(L_ITEM) = item;
                             LI(L_BLEFT) = P->ss.batch_size;
-                            sample = 0;
+                            LI(L_SAMPLE) = 0u;
                         }
                         advance();
                     }
@@ -975,46 +992,45 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #endif
             if (!leaf_pass) {
                 if (tracing && !at_leaf) {
-                    // One 64-B record (4 x dwordx4 off the SGPR base, offset = cur << 6), the
+                    // One 32-B record (2 x 16 B off the SGPR base, offset = cur << 5), the
                     // box test, and the next record: the hit link or the miss link.
-                    DNode nd;
-                    if (cur < A.lds_top) {
-                        nd = load_node56_lds(s_top + (cur << 6));
-                    } else {
-                        nd = load_node56((const DNode*)((const char*)A.nodes + (cur << 6)));
-                    }
+                    u32x4 ra, rb;
+                    load_tnode(s_nodes, A.tnodes, cur, A.lds_nodes, ra, rb);
                     c_nodes++;
                     bool h;
                     if (wave_fast) {
-                        h = box_hit_fast(nd, ray.o, inv, tmin, closest);
-                    } else {
-                        h = box_hit(nd, ray.o, inv, tmin, closest);
+                        bool undecided;
+                        h = box_cert(__uint_as_float(ra.x), __uint_as_float(ra.y), __uint_as_float(ra.z),
+                                     __uint_as_float(ra.w), __uint_as_float(rb.x), __uint_as_float(rb.y), rc, tmin32,
+                                     closest32, undecided);
+                        if (undecided) {  // undecided by f32 (rare): the reference's f64 test
+                            h = box_hit_fast(box64(A.tboxes[cur]), ray.o, inv_of(ray.d), tmin, closest);
+                        }
+                    } else {  // a wave with a non-cert ray: the f64 compare-select test
+                        h = box_hit(box64(A.tboxes[cur]), ray.o, inv_of(ray.d), tmin, closest);
                     }
-                    cur = h ? nd.left : nd.right;
+                    cur = h ? rb.z : rb.w;
                 }
             } else if (at_leaf) {
                 double scx, scy, scz, sr;
                 uint32_t next, ref;
-                const uint32_t li = cur & ~THR_LEAF;
-                if (li < A.lds_top) {
-                    load_leaf_rec_lds(s_top + (li << 6), scx, scy, scz, sr, next, ref);
-                } else {
-                    load_leaf_rec((const DNode*)((const char*)A.nodes + (li << 6)), scx, scy, scz, sr, next, ref);
-                }
+                load_tleaf(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr, next, ref);
                 if ((ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {  // a stationary sphere, inline
                     c_sph++;
                     double t;
                     if (sphere_accept(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
                         closest = t;
+                        closest32 = (float)t;
                         hit_ref = ref;
-                        hit_inst = GS_REF_NONE;
+                        LI(L_HINST) = GS_REF_NONE;
                     }
                 } else {
                     const LeafHit lh = leaf_other<FEAT>(sc, ref, ray, tmin, closest, rng, s_cnt);
                     if (lh.hit) {
                         closest = lh.t;
+                        closest32 = (float)lh.t;
                         hit_ref = lh.ref;
-                        hit_inst = lh.inst;
+                        LI(L_HINST) = lh.inst;
                     }
                 }
                 cur = next;
@@ -1028,19 +1044,15 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 // instances) lose ~2% to the loop's mere presence (MI355X C3).
 #pragma unroll 1
                 for (int k = 1; (FEAT & GS_FEAT_LEAFRUN) && k < GS_LEAF_RUN && cur > THR_END; k++) {
-                    const uint32_t l2 = cur & ~THR_LEAF;
-                    if (l2 < A.lds_top) {
-                        load_leaf_rec_lds(s_top + (l2 << 6), scx, scy, scz, sr, next, ref);
-                    } else {
-                        load_leaf_rec((const DNode*)((const char*)A.nodes + (l2 << 6)), scx, scy, scz, sr, next, ref);
-                    }
+                    load_tleaf(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr, next, ref);
                     if ((ref >> GS_REF_SHIFT) != GS_REF_SPHERE) break;
                     c_sph++;
                     double t;
                     if (sphere_accept(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
                         closest = t;
+                        closest32 = (float)t;
                         hit_ref = ref;
-                        hit_inst = GS_REF_NONE;
+                        LI(L_HINST) = GS_REF_NONE;
                     }
                     cur = next;
                 }
@@ -1074,7 +1086,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             } else {
                 atomicAdd(&s_cnt[C_HITS], 1ull);
                 GS_STAMP(r0);
-                const HitRec h = reconstruct(sc, ray, closest, hit_ref, hit_inst);
+                const HitRec h = reconstruct(sc, ray, closest, hit_ref, LI(L_HINST));
                 GS_REGION(1, r0);
                 GS_STAMP(r0);
                 const Scatter s = scatter(sc, h, ray.d, rng, s_cnt);
@@ -1084,7 +1096,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     Tr = Tr * s.col.x;
                     Tg = Tg * s.col.y;
                     Tb = Tb * s.col.z;
-                    depth--;
+                    const uint32_t depth = LI(L_DEPTH) - 1u;
+                    LI(L_DEPTH) = depth;
                     if (depth > 0) {
                         ray.o = h.p;
                         ray.d = s.dir;
@@ -1203,17 +1216,17 @@ static thread_local std::string tl_err;
 static int32_t g_shade_batch = 52;  // swept on MI355X C4 (chunked, uniform loop): 48 -> 3502, 52 -> 3535-3568, 56 -> 3506-3536 Msamples/s
 static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
 static int32_t g_leaf_batch = 12;  // swept on MI355X C4 with leaf runs: 8 -> 4586, 10 -> 4632, 12 -> 4648-4651, 14 -> 4624, 16 -> 4592
-// Threaded records mirrored in LDS per block (the shallowest ones): what is left of the
-// block's share of the CU's 160 KiB (4 waves/SIMD = 1024 lanes per CU) after the lane
-// state.  256-lane blocks: 352 records.  -1 = that budget; >= 0 explicit (A/B).
-#ifndef GS_LDS_TOP
-#define GS_LDS_TOP -1
+// Bytes of threaded records mirrored in LDS per block (the most-tested ones): what is
+// left of the block's share of the CU's 160 KiB (4 waves/SIMD = 1024 lanes per CU) after
+// the lane state.  -1 = that budget; >= 0 explicit (A/B).
+#ifndef GS_LDS_MIRROR
+#define GS_LDS_MIRROR -1
 #endif
-static int32_t g_lds_top = GS_LDS_TOP;
-static uint32_t lds_top_budget() {
+static int64_t g_lds_mirror = GS_LDS_MIRROR;
+static int64_t lds_mirror_budget() {
     const int64_t share = (int64_t)160 * 1024 * GS_BLOCK / 1024;
     const int64_t left = share - (int64_t)GS_BLOCK * (L_ND * 8 + L_NI * 4) - 1024;  // 1 KiB: static LDS + slack
-    return left > 0 ? (uint32_t)(left / 64) : 0u;
+    return left > 0 ? left : 0;
 }
 // -1 auto, 0 never split a pixel's samples.  Swept on MI355X with batched queue claims,
 // C4 rank 0 / rank 3 of N (tools/rank_sim.py; ms): N=1: 4 -> 658.4, 8 -> 658.7,
@@ -1254,17 +1267,20 @@ struct gs_device_scene {
     DevScene dev{};
     uint32_t n_nodes = 0;
     uint32_t bvh_depth = 1;  // top-level BVH depth (informational: the walk keeps no stack)
-    bool fast_boxes = false;  // every node coordinate |x| < 1e300
+    bool cert_boxes = false;  // every top-level node coordinate |x| <= 1e15 (box_cert applies)
     int feat = 0;             // GS_FEAT_* of the kernel instantiation to launch
-    const DNode* thr = nullptr;  // threaded top-level records (THR_END)
+    // The threaded top-level tree (THR_*): node records, their f64 boxes, leaf records.
+    const TNode* tnodes = nullptr;
+    const TBox* tboxes = nullptr;
+    const TLeaf* tleaves = nullptr;
     uint32_t thr_root = THR_END;
-    uint32_t lds_top = 0;        // records mirrored in LDS per block
+    uint32_t lds_nodes = 0, lds_leaves = 0;  // mirrored prefixes (per block)
     // Launch state, mutated by launches of a const scene: guarded by `mu`.
     std::mutex mu;
     // launch geometry, computed at the first launch (host API queries cost ~0.5 ms each)
     bool launch_ready = false;
     int cus = 0, per_cu = 0;
-    uint32_t launch_lds_top = 0;
+    uint32_t launch_lds_nodes = 0, launch_lds_leaves = 0;
     size_t launch_lds = 0;
     LaunchSlot slots[kLaunchSlots];
     uint32_t next_slot = 0;
@@ -1519,10 +1535,13 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                          device_ref(n.left), device_ref(n.right), 0, 0};
     }
     // The threaded top-level tree (see THR_END): pre-order records of nodes and leaf
-    // occurrences; raw links first, tagged once every record's kind is known.
+    // occurrences; raw links first, then split into node and leaf arrays.
     std::vector<DNode> thr;
     std::vector<uint8_t> thr_leaf;
-    uint32_t lds_top = 0, thr_root_tagged = THR_END;
+    std::vector<TNode> tnodes;
+    std::vector<TBox> tboxes;
+    std::vector<TLeaf> tleaves;
+    uint32_t lds_nodes = 0, lds_leaves = 0, thr_root_tagged = THR_END;
     bool leaf_runs = false;
     {
         // Iterative pre-order: a node pushes a "close" marker below its children, which
@@ -1570,8 +1589,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             std::vector<uint32_t> depth(n, 0), order;
             for (uint32_t i = 0; i < n; i++)
                 if (!thr_leaf[i]) {
-                    if (thr[i].left < n) depth[thr[i].left] = depth[i] + 1;  // records are pre-order:
-                    // a node's descendants follow it, so depths propagate in one forward pass
+                    // records are pre-order: a node's descendants follow it, so depths
+                    // propagate in one forward pass
                     for (uint32_t c = thr[i].left; c < thr[i].right && c < n;) {
                         depth[c] = depth[i] + 1;
                         c = thr_leaf[c] ? c + 1 : thr[c].right;  // next child of node i
@@ -1579,7 +1598,6 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                 }
             order.resize(n);
             for (uint32_t i = 0; i < n; i++) order[i] = i;
-            const uint32_t k = std::min<uint32_t>(n, g_lds_top < 0 ? lds_top_budget() : (uint32_t)g_lds_top);
             // score = surface area of the parent's box (the chance a ray tests the record)
             std::vector<double> score(n, 0.0);
             if (n) score[0] = 1e308;
@@ -1596,23 +1614,43 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
                 return score[a] > score[b] || (score[a] == score[b] && depth[a] < depth[b]);
             });
+            // Fill the LDS byte budget in that order (32-B node records, 48-B leaf records).
+            const int64_t budget = g_lds_mirror < 0 ? lds_mirror_budget() : g_lds_mirror;
             std::vector<uint8_t> top(n, 0);
-            for (uint32_t i = 0; i < k; i++) top[order[i]] = 1;
-            uint32_t next_top = 0, next_rest = k;
-            for (uint32_t i = 0; i < n; i++) pos[i] = top[i] ? next_top++ : next_rest++;
-            lds_top = k;
+            int64_t used = 0;
+            for (uint32_t i = 0; i < n; i++) {
+                const uint32_t r = order[i];
+                const int64_t sz = thr_leaf[r] ? (int64_t)sizeof(TLeaf) : (int64_t)sizeof(TNode);
+                if (used + sz > budget) {
+                    if (used + (int64_t)sizeof(TNode) > budget) break;
+                    continue;
+                }
+                used += sz;
+                top[r] = 1;
+                (thr_leaf[r] ? lds_leaves : lds_nodes)++;
+            }
+            uint32_t nt = 0, nl = 0, nt_rest = lds_nodes, nl_rest = lds_leaves;
+            for (uint32_t i = 0; i < n; i++) {
+                if (thr_leaf[i]) pos[i] = top[i] ? nl++ : nl_rest++;
+                else pos[i] = top[i] ? nt++ : nt_rest++;
+            }
+            tnodes.resize(nt_rest);
+            tboxes.resize(nt_rest);
+            tleaves.resize(nl_rest);
         }
-        auto tag = [&](uint32_t l) {
-            return l >= n ? THR_END : (thr_leaf[l] ? (THR_LEAF | pos[l]) : pos[l]);
-        };
-        std::vector<DNode> placed(n);
+        auto tag = [&](uint32_t l) { return l >= n ? THR_END : (thr_leaf[l] ? (THR_LEAF | pos[l]) : pos[l]); };
         for (uint32_t i = 0; i < n; i++) {
-            DNode r = thr[i];
-            r.left = tag(r.left);
-            if (!thr_leaf[i]) r.right = tag(r.right);  // a leaf's `right` is its ref
-            placed[pos[i]] = r;
+            const DNode& r = thr[i];
+            if (thr_leaf[i]) {
+                tleaves[pos[i]] = TLeaf{r.mnx, r.mny, r.mnz, r.mxx, tag(r.left), r.right, 0u, 0u};
+            } else {
+                // f32 box coordinates rounded to nearest (the certified test's error model)
+                tnodes[pos[i]] = TNode{(float)r.mnx, (float)r.mny, (float)r.mnz, (float)r.mxx, (float)r.mxy,
+                                       (float)r.mxz, tag(r.left), tag(r.right)};
+                tboxes[pos[i]] = TBox{r.mnx, r.mny, r.mnz, r.mxx, r.mxy, r.mxz};
+            }
         }
-        thr_root_tagged = n == 0 ? THR_END : (thr_leaf[0] ? (THR_LEAF | pos[0]) : pos[0]);
+        thr_root_tagged = n == 0 ? THR_END : tag(0);
         // Leaf runs pay when at least a quarter of the leaf records are the first of two
         // adjacent sphere leaves (C4's two-sphere leaves of BVH.rs:44-55: ~half).
         {
@@ -1624,9 +1662,13 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             }
             leaf_runs = leaves && pairs * 4 >= leaves;
         }
-        thr.swap(placed);
     }
-    if (thr.size() >= (1u << 26)) return fail(GS_ERR_UNSUPPORTED, "more than 2^26 top-level BVH records");
+    if (tnodes.size() >= (1u << 26) || tleaves.size() >= (1u << 26))
+        return fail(GS_ERR_UNSUPPORTED, "more than 2^26 top-level BVH records");
+    bool cert_boxes = true;
+    for (const TBox& b : tboxes)
+        for (double v : {b.mnx, b.mny, b.mnz, b.mxx, b.mxy, b.mxz})
+            if (!(std::fabs(v) <= 1e15)) cert_boxes = false;
     std::vector<DSphere> sph(s->n_spheres);
     std::vector<uint32_t> sph_mat(s->n_spheres);
     for (uint32_t i = 0; i < s->n_spheres; i++) {
@@ -1682,7 +1724,9 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     }
     Layout L;
     size_t o_nodes = L.add(nodes.data(), nodes.size() * sizeof(DNode));
-    size_t o_thr = L.add(thr.data(), thr.size() * sizeof(DNode));
+    size_t o_tnodes = L.add(tnodes.data(), tnodes.size() * sizeof(TNode));
+    size_t o_tboxes = L.add(tboxes.data(), tboxes.size() * sizeof(TBox));
+    size_t o_tleaves = L.add(tleaves.data(), tleaves.size() * sizeof(TLeaf));
     size_t o_sph = L.add(sph.data(), sph.size() * sizeof(DSphere));
     size_t o_sphm = L.add(sph_mat.data(), sph_mat.size() * 4);
     size_t o_msph = L.add(s->mspheres, s->n_mspheres * sizeof(gs_msphere));
@@ -1745,15 +1789,15 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         }
     }
     ds->n_nodes = s->n_nodes;
-    ds->thr = (const DNode*)(b + o_thr);
+    ds->tnodes = (const TNode*)(b + o_tnodes);
+    ds->tboxes = (const TBox*)(b + o_tboxes);
+    ds->tleaves = (const TLeaf*)(b + o_tleaves);
     ds->thr_root = thr_root_tagged;
-    ds->lds_top = lds_top;
+    ds->lds_nodes = lds_nodes;
+    ds->lds_leaves = lds_leaves;
     ds->bvh_depth = depth < 1 ? 1 : depth;
     ds->feat = (s->n_media != 0 ? GS_FEAT_MEDIA : 0) | (nested ? GS_FEAT_NESTED : 0) | (leaf_runs ? GS_FEAT_LEAFRUN : 0);
-    ds->fast_boxes = true;
-    for (uint32_t i = 0; i < s->n_nodes && ds->fast_boxes; i++)
-        for (int k = 0; k < 3; k++)
-            if (!(std::fabs(s->nodes[i].min[k]) < 1e300 && std::fabs(s->nodes[i].max[k]) < 1e300)) ds->fast_boxes = false;
+    ds->cert_boxes = cert_boxes;
     *out = ds;
     return GS_OK;
 }
@@ -1869,9 +1913,11 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     kp.counters = (unsigned long long*)d_counters;
     kp.item_visits = outs->item_visits;
     KArgs a{};
-    a.nodes = ds->thr;
+    a.tnodes = ds->tnodes;
+    a.tboxes = ds->tboxes;
+    a.tleaves = ds->tleaves;
     a.root = ds->thr_root;
-    a.fast_boxes = ds->fast_boxes ? 1 : 0;
+    a.cert_boxes = ds->cert_boxes ? 1 : 0;
     a.shade_batch = g_shade_batch;
     a.leaf_batch = g_leaf_batch < 1 ? 1 : g_leaf_batch;  // 0 would never step a node
     gs_device_scene* mds = const_cast<gs_device_scene*>(ds);
@@ -1879,15 +1925,21 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     if (!mds->launch_ready) {
         HIPCHK(hipDeviceGetAttribute(&mds->cus, hipDeviceAttributeMultiprocessorCount, dev));
         // The mirror takes what the block's LDS limit leaves after the kernel's static LDS
-        // and the lane state (records [0, lds_top) are the best ones, so any prefix is valid).
+        // and the lane state (any prefix of either record array is a valid mirror).
         hipFuncAttributes fa{};
         HIPCHK(hipFuncGetAttributes(&fa, (const void*)kernel_for(ds->feat)));
         int max_lds = 0;
         HIPCHK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
         const int64_t room = (int64_t)max_lds - (int64_t)fa.sharedSizeBytes - (int64_t)lane_lds_bytes();
         if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
-        mds->launch_lds_top = std::min<uint32_t>(ds->lds_top, (uint32_t)(room / (int64_t)sizeof(DNode)));
-        mds->launch_lds = lane_lds_bytes() + (size_t)mds->launch_lds_top * sizeof(DNode);
+        uint32_t ln = ds->lds_nodes, ll = ds->lds_leaves;
+        while ((int64_t)ln * (int64_t)sizeof(TNode) + (int64_t)ll * (int64_t)sizeof(TLeaf) > room) {
+            if (ln) ln = ln - 1 - ln / 16;  // shrink both prefixes until they fit
+            if (ll) ll = ll - 1 - ll / 16;
+        }
+        mds->launch_lds_nodes = ln;
+        mds->launch_lds_leaves = ll;
+        mds->launch_lds = lane_lds_bytes() + (size_t)ln * sizeof(TNode) + (size_t)ll * sizeof(TLeaf);
         int occ = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel_for(ds->feat), GS_BLOCK, mds->launch_lds));
         mds->per_cu = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
@@ -1895,7 +1947,8 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     }
     const int cus = ds->cus;
     const size_t lds = ds->launch_lds;
-    a.lds_top = ds->launch_lds_top;
+    a.lds_nodes = ds->launch_lds_nodes;
+    a.lds_leaves = ds->launch_lds_leaves;
     const int per_cu = g_blocks_per_cu > 0 ? g_blocks_per_cu : ds->per_cu;
     int64_t blocks = (int64_t)cus * per_cu;
     // no more waves than work: one lane per item at most

@@ -24,6 +24,33 @@ __global__ void k_aabb(int n, const double* box, const double* ray, const double
     out[i] = box_hit(nd, o, inv, iv[2 * i], iv[2 * i + 1]) ? 1 : 0;
 }
 
+// The megakernel's node decision for cert rays: box_cert (f32, certified), and the f64
+// box_hit_fast where box_cert is undecided.  out: 0/1 the decision, dec: 0 miss / 1 hit
+// certified by f32, 2 undecided; -1 for rays that are not cert rays (not decided here).
+__global__ void k_aabb_cert(int n, const double* box, const double* ray, const double* iv, int* out, int* dec) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double* b = box + 6 * i;
+    DNode nd{b[0], b[1], b[2], b[3], b[4], b[5], 0, 0, 0, 0};
+    d3 o = mk(ray[6 * i], ray[6 * i + 1], ray[6 * i + 2]);
+    d3 d = mk(ray[6 * i + 3], ray[6 * i + 4], ray[6 * i + 5]);
+    d3 inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+    bool boxes_ok = true;
+    for (int k = 0; k < 6; k++) boxes_ok = boxes_ok && __builtin_fabs(b[k]) <= 1e15;
+    if (!boxes_ok || !cert_ray_ok(o, inv)) {
+        out[i] = -1;
+        dec[i] = -1;
+        return;
+    }
+    const RayCert rc = make_cert(o, inv);
+    bool und;
+    bool h = box_cert((float)b[0], (float)b[1], (float)b[2], (float)b[3], (float)b[4], (float)b[5], rc,
+                      (float)iv[2 * i], (float)iv[2 * i + 1], und);
+    dec[i] = und ? 2 : (h ? 1 : 0);
+    if (und) h = box_hit_fast(nd, o, inv, iv[2 * i], iv[2 * i + 1]);
+    out[i] = h ? 1 : 0;
+}
+
 __global__ void k_sphere(int n, const double* sph, const double* ray, const double* iv, double* t, int* hit) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -117,6 +144,17 @@ int kat_aabb(int n, const double* box, const double* ray, const double* iv, int*
     int* dout = dcopy<int>(nullptr, n);
     hipLaunchKernelGGL(k_aabb, grid(n), dim3(256), 0, 0, n, db, dr, di, dout);
     back(out, dout, n);
+    (void)hipFree(db); (void)hipFree(dr); (void)hipFree(di);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+int kat_aabb_cert(int n, const double* box, const double* ray, const double* iv, int* out, int* dec) {
+    double *db = dcopy(box, 6 * (size_t)n), *dr = dcopy(ray, 6 * (size_t)n), *di = dcopy(iv, 2 * (size_t)n);
+    int* dout = dcopy<int>(nullptr, n);
+    int* ddec = dcopy<int>(nullptr, n);
+    hipLaunchKernelGGL(k_aabb_cert, grid(n), dim3(256), 0, 0, n, db, dr, di, dout, ddec);
+    back(out, dout, n);
+    back(dec, ddec, n);
     (void)hipFree(db); (void)hipFree(dr); (void)hipFree(di);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }

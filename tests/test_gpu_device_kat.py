@@ -18,7 +18,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 def kat(built):
     L = C.CDLL(os.path.join(HERE, "hip", "libkat_device.so"))
     P = C.c_void_p
-    for f, args in {"kat_aabb": [C.c_int, P, P, P, P], "kat_sphere": [C.c_int, P, P, P, P, P],
+    for f, args in {"kat_aabb": [C.c_int, P, P, P, P], "kat_aabb_cert": [C.c_int, P, P, P, P, P],
+                    "kat_sphere": [C.c_int, P, P, P, P, P],
                     "kat_tri": [C.c_int, P, P, P, P], "kat_rng": [C.c_int, P, P, P, C.c_int, P],
                     "kat_math": [C.c_int, C.c_int, P, P, P],
                     "kat_noise": [C.c_int, C.c_int, P, C.c_double, P, P]}.items():
@@ -64,6 +65,58 @@ def test_aabb_matches_oracle(kat):
                     for i in range(n)], np.int32)
     assert np.array_equal(out, ref)
     assert 0.05 < out.mean() < 0.95  # both outcomes exercised
+
+
+def _grazing_cases(rng, n):
+    """Rays aimed at box edges, faces and corners (tiny offsets, where f32 cannot decide),
+    at unit and at C4 scales (boxes up to 2000 wide, origins up to 60 away)."""
+    scale = np.where(rng.random(n) < 0.5, 1.0, rng.uniform(1, 60, n))[:, None]
+    lo = rng.uniform(-3, 2, (n, 3)) * scale
+    ext = rng.uniform(0.01, 3, (n, 3)) * np.where(rng.random((n, 1)) < 0.1, 700.0, 1.0) * scale
+    box = np.hstack([lo, lo + ext])
+    o = rng.uniform(-6, 6, (n, 3)) * scale
+    # a target on the box surface: a corner, an edge or a face point, nudged by +-ulps
+    t = lo + ext * rng.integers(0, 2, (n, 3))
+    face = rng.integers(0, 3, n)
+    frac = rng.random((n, 3))
+    for k in range(3):
+        m = (face == k) & (rng.random(n) < 0.5)
+        t[m, k] = lo[m, k] + ext[m, k] * frac[m, k]
+    t = t * (1.0 + rng.choice([-1, 1], (n, 3)) * rng.choice([0.0, 1e-16, 1e-12, 1e-9, 1e-7, 1e-5], (n, 3)))
+    d = t - o
+    d = d / np.where(rng.random((n, 1)) < 0.5, 1.0, np.linalg.norm(d, axis=1, keepdims=True))
+    ray = np.hstack([o, d])
+    tmax = np.where(rng.random(n) < 0.6, 1.7976931348623157e308, rng.uniform(0.2, 3.0, n))
+    iv = np.stack([np.full(n, 0.001), tmax], 1)
+    return np.ascontiguousarray(box), np.ascontiguousarray(ray), np.ascontiguousarray(iv)
+
+
+def test_certified_f32_slab_matches_oracle(kat):
+    """The node test the kernel runs for cert rays (box_cert in f32, the f64 test where it
+    is undecided) decides exactly as the reference's f64 AABB::hit, on random boxes and
+    on rays grazing box corners / edges / faces by 1e-16 .. 1e-5 relative; every
+    decision f32 certifies is correct, and undecided ones are rare on random rays."""
+    rng = np.random.default_rng(11)
+    n = 40000
+    box, ray, iv = _grazing_cases(rng, n)
+    # plus the random cases of test_aabb_matches_oracle (non-cert rays report -1)
+    rb = rng.uniform(-3, 2, (n, 3))
+    box = np.ascontiguousarray(np.vstack([box, np.hstack([rb, rb + rng.uniform(0.1, 3, (n, 3))])]))
+    ray = np.ascontiguousarray(np.vstack([ray, _rays(rng, n)]))
+    iv = np.ascontiguousarray(np.vstack([iv, np.stack([np.full(n, 0.001), rng.uniform(0, 6, n)], 1)]))
+    m = 2 * n
+    out = np.zeros(m, np.int32)
+    dec = np.zeros(m, np.int32)
+    assert kat.kat_aabb_cert(m, ptr(box), ptr(ray), ptr(iv), ptr(out), ptr(dec)) == 0
+    ref = np.array([oracle.aabb_hit(box[i, :3], box[i, 3:], ray[i, :3], ray[i, 3:], iv[i, 0], iv[i, 1])
+                    for i in range(m)], np.int32)
+    cert = dec >= 0
+    assert cert[:n].all() and 0.4 < cert[n:].mean() < 1.0  # grazing cases are cert rays; the zero / -0 direction cases are not
+    assert np.array_equal(out[cert], ref[cert])
+    sure = (dec == 0) | (dec == 1)
+    assert np.array_equal(dec[sure], ref[sure])  # what f32 certifies is right
+    assert (dec[:n] == 2).sum() > 50  # the grazing cases do reach the f64 fallback
+    assert (dec[n:][cert[n:]] == 2).mean() < 1e-3  # and random rays almost never need it
 
 
 def test_sphere_matches_oracle_bitwise(kat):
