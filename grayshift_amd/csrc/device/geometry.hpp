@@ -64,41 +64,16 @@ __device__ __forceinline__ DNode load_node56(const DNode* p) {
 // non-NaN values are ever assigned) and IEEE maxNum ignores a NaN operand, as the
 // reference's failed comparison does (a == lo keeps an equal value).  Same for hi.
 // The t0/t1 swap must stay a compare-select: min/max would treat a NaN t1 differently.
-// v_max_f64 / v_min_f64 as they are: IEEE maxNum / minNum, a quiet-NaN operand yields
-// the other one.  fmax/fmin would first "canonicalize" operands the compiler cannot
-// prove are not signalling NaNs (a v_max x,x each); these operands are results of f64
-// arithmetic or the interval bounds, never sNaN, so the bare instruction is the same
-// function.
-__device__ __forceinline__ double hw_max(double a, double b) {
-#ifndef GS_NO_ASM_MINMAX
-    double r;
-    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-#else
-    return fmax(a, b);
-#endif
-}
-__device__ __forceinline__ double hw_min(double a, double b) {
-#ifndef GS_NO_ASM_MINMAX
-    double r;
-    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-#else
-    return fmin(a, b);
-#endif
-}
-
-// max(u, b) with a wave-uniform u (tmin) taken as an SGPR-pair operand, so the constant
-// is not rematerialised into VGPRs every traversal step.
-__device__ __forceinline__ double hw_max_u(double u, double b) {
-#ifndef GS_NO_ASM_MINMAX
-    double r;
-    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "s"(u), "v"(b));
-    return r;
-#else
-    return fmax(u, b);
-#endif
-}
+// (Round 1 issued bare v_max_f64 / v_min_f64 through inline asm, one with an SGPR-pair
+// operand.  With the certified f32 test added, the media + nested-BVH kernel — which
+// spills SGPRs and VGPRs — rendered final_scene wrongly and non-deterministically with
+// the asm and correctly with these builtins (every node decision checked right, so the
+// asm's operands were corrupted; a hazard the compiler does not guard inside inline asm
+// is the likely cause).  The f64 test is now the rare path behind box_cert, so the
+// builtins' canonicalisation costs nothing measurable.)
+__device__ __forceinline__ double hw_max(double a, double b) { return __builtin_fmax(a, b); }
+__device__ __forceinline__ double hw_min(double a, double b) { return __builtin_fmin(a, b); }
+__device__ __forceinline__ double hw_max_u(double u, double b) { return __builtin_fmax(u, b); }
 
 __device__ __forceinline__ void slab(double mn, double mx, double o, double inv, double& lo, double& hi) {
     const double t0 = (mn - o) * inv, t1 = (mx - o) * inv;

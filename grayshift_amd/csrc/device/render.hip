@@ -178,7 +178,9 @@ __host__ __device__ inline uint32_t device_ref(uint32_t abi_ref) {
 #define THR_LEAF 0x80000000u
 
 // Node and leaf records live in two arrays (32-B TNode, 48-B TLeaf: geometry.hpp); a link
-// is a node index, THR_LEAF | a leaf index, or THR_END.  Each block mirrors the most-tested
+// is a node's byte offset (index << 5: the address arithmetic of a node step is then
+// none in LDS and one SGPR-base add in global memory), THR_LEAF | a leaf index, or
+// THR_END.  Each block mirrors the most-tested
 // prefix of both arrays in LDS.  Address-space-qualified pointers keep the mirror reads
 // ds_read instructions: a select between an LDS and a global pointer would compile to
 // flat loads, which measured 34% slower on the whole kernel.
@@ -188,16 +190,18 @@ typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
 typedef __attribute__((address_space(3))) const u32x2 lds_u32x2;
 __device__ __forceinline__ double lo_hi(unsigned int lo, unsigned int hi) { return __hiloint2double((int)hi, (int)lo); }
 
-// A node record (2 x 16 B): a = (mnx, mny, mnz, mxx), b = (mxy, mxz, hit, miss).
-// (Offsets are u32: indices < 2^26, so i * 48 < 2^32 — one SGPR base + a 32-bit VGPR offset.)
-__device__ __forceinline__ void load_tnode(const uint8_t* s_nodes, const TNode* g, uint32_t i, uint32_t lds_n,
+// A node record (2 x 16 B) at byte offset `off`: a = (mnx, mny, mnz, mxx), b = (mxy, mxz,
+// hit, miss).  (Offsets are u32: fewer than 2^26 records; leaf offsets i * 48 < 2^32.)
+__device__ __forceinline__ void load_tnode(const uint8_t* s_nodes, const TNode* g, uint32_t off, uint32_t lds_bytes,
                                            u32x4& a, u32x4& b) {
-    if (i < lds_n) {
-        lds_u32x4* q = (lds_u32x4*)(s_nodes + (i << 5));
+    if (off < lds_bytes) {
+        // The kernel has no static LDS (checked at launch), so the node mirror's first byte
+        // is LDS address 0 and `off` is the record's LDS address (no address arithmetic).
+        lds_u32x4* q = (lds_u32x4*)(uintptr_t)off;
         a = q[0];
         b = q[1];
     } else {
-        const u32x4* q = reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(g) + (i << 5));
+        const u32x4* q = reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(g) + off);
         a = q[0];
         b = q[1];
     }
@@ -207,7 +211,9 @@ __device__ __forceinline__ void load_tnode(const uint8_t* s_nodes, const TNode* 
 // registers live across the whole loop: recomputed where needed, they cost nothing in
 // the common path.
 __device__ __forceinline__ d3 inv_of(d3 d) {
+#ifndef GS_NO_INV_BARRIER
     asm volatile("" : "+v"(d.x), "+v"(d.y), "+v"(d.z));
+#endif
     return mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
 }
 // A leaf record: the sphere's centre and radius, its next link and its ABI ref.
@@ -680,22 +686,29 @@ enum { L_CSR = 0, L_CSG, L_CSB, L_LSUM, L_LSQ, L_SCOUNT, L_ND };
 enum { L_ITEM = 0, L_PIX, L_BLEFT, L_SAMPLE, L_DEPTH, L_HINST, L_NI };  // (sample, depth, hit
 // instance: per-path state touched once per bounce, kept out of the traversal loop's VGPRs)
 
-__host__ __device__ constexpr size_t lane_lds_bytes() { return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4); }
+// Lane state plus the block's 64-bit counters (C_N of them, 128 B).  There is no static
+// LDS: the dynamic LDS then starts at address 0, so a node's LDS address is its byte
+// offset itself (node links are pre-shifted, below).
+#ifdef GS_STAMPS
+#define GS_STAMP_LDS ((GS_BLOCK / 64) * 8 * 8)
+#else
+#define GS_STAMP_LDS 0
+#endif
+__host__ __device__ constexpr size_t lane_lds_bytes() {
+    return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4) + 128 + GS_STAMP_LDS;
+}
 
 template <int FEAT>
 __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs A) {
     extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ unsigned long long s_cnt[C_N];
 #ifdef GS_STAMPS
-    __shared__ unsigned long long s_reg[(GS_BLOCK / 64) * 8];
-    if (threadIdx.x < (GS_BLOCK / 64) * 8) s_reg[threadIdx.x] = 0;
 #endif
-    double* s_d = (double*)smem;                                  // [L_ND][GS_BLOCK]
-    uint32_t* s_i = (uint32_t*)(smem + L_ND * 8 * GS_BLOCK);      // [L_NI][GS_BLOCK]
+
     // The records a ray most likely tests (placed first by the host) are mirrored in LDS;
     // a lane whose node / leaf index is below lds_nodes / lds_leaves reads it from there
-    // (ds_read), the rest from global memory.
-    uint8_t* s_nodes = smem + lane_lds_bytes();
+    // (ds_read), the rest from global memory.  The node mirror starts the dynamic LDS, so
+    // a node's LDS address is cur << 5 plus a constant the ds_read offset absorbs.
+    uint8_t* s_nodes = smem;
     uint8_t* s_leaves = s_nodes + (size_t)A.lds_nodes * sizeof(TNode);
     {
         const uint4* src = reinterpret_cast<const uint4*>(A.tnodes);
@@ -705,6 +718,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         dst = reinterpret_cast<uint4*>(s_leaves);
         for (uint32_t k = threadIdx.x; k < A.lds_leaves * 3u; k += GS_BLOCK) dst[k] = src[k];
     }
+    // Per-lane pixel / path state after the mirror: [L_ND][GS_BLOCK] f64, [L_NI][GS_BLOCK] u32.
+    double* s_d = (double*)(s_leaves + (size_t)A.lds_leaves * sizeof(TLeaf));
+    uint32_t* s_i = (uint32_t*)(s_d + L_ND * GS_BLOCK);
+    unsigned long long* s_cnt = (unsigned long long*)(s_i + L_NI * GS_BLOCK);
+#ifdef GS_STAMPS
+    unsigned long long* s_reg = s_cnt + 16;  // [(GS_BLOCK / 64) * 8]
+    if (threadIdx.x < (GS_BLOCK / 64) * 8) s_reg[threadIdx.x] = 0;
+#endif
     if (threadIdx.x < C_N) s_cnt[threadIdx.x] = 0;
     __syncthreads();
 
@@ -969,19 +990,25 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         // shade count and the slab flavour are wave-uniform SGPR facts: no per-iteration
         // ballot for the former, a scalar branch (no exec-mask juggling) for the latter.
         const uint64_t alive = __builtin_amdgcn_ballot_w64(st != S_DONE);
+#ifdef GS_NO_CERT
+        const bool wave_fast = false;
+#else
         const bool wave_fast = __builtin_amdgcn_ballot_w64(st == S_TRACE && !fast) == 0;
+#endif
+        // Invariant: cur != THR_END exactly for lanes whose ray is still being traced
+        // (every other lane holds THR_END), so the loop reads lane states from `cur` alone
+        // and only marks finished lanes S_SHADE once it ends.
 #pragma unroll 1
         for (;;) {
-            const bool tracing = st == S_TRACE;
-            const uint64_t tr = __builtin_amdgcn_ballot_w64(tracing);
+            const uint64_t tr = __builtin_amdgcn_ballot_w64(cur != THR_END);
             if (tr == 0) break;
             if ((uint32_t)__popcll(alive & ~tr) >= (uint32_t)A.shade_batch) break;
             // Leaf batching: step nodes until `leaf_batch` tracing lanes sit at a leaf (or all
             // do), then test those leaves together, so a wave pays for the node step and the
             // sphere test in different iterations instead of both in every one.  Each lane
             // still processes its refs in the reference's order.  The pass kind is uniform.
-            const bool at_leaf = tracing && cur > THR_END;
-            const uint64_t lm = tr & __builtin_amdgcn_ballot_w64(cur > THR_END);  // == ballot(at_leaf)
+            const bool at_leaf = cur > THR_END;
+            const uint64_t lm = __builtin_amdgcn_ballot_w64(at_leaf);
             const bool leaf_pass = lm == tr || (uint32_t)__popcll(lm) >= (uint32_t)A.leaf_batch;
 #ifdef GS_STAMPS
             it_all++;
@@ -991,11 +1018,11 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             ln_leaf += leaf_pass ? (uint64_t)__popcll(lm) : 0ull;
 #endif
             if (!leaf_pass) {
-                if (tracing && !at_leaf) {
+                if (cur < THR_END) {
                     // One 32-B record (2 x 16 B off the SGPR base, offset = cur << 5), the
                     // box test, and the next record: the hit link or the miss link.
                     u32x4 ra, rb;
-                    load_tnode(s_nodes, A.tnodes, cur, A.lds_nodes, ra, rb);
+                    load_tnode(s_nodes, A.tnodes, cur, A.lds_nodes << 5, ra, rb);
                     c_nodes++;
                     bool h;
                     if (wave_fast) {
@@ -1004,10 +1031,29 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                                      __uint_as_float(ra.w), __uint_as_float(rb.x), __uint_as_float(rb.y), rc, tmin32,
                                      closest32, undecided);
                         if (undecided) {  // undecided by f32 (rare): the reference's f64 test
-                            h = box_hit_fast(box64(A.tboxes[cur]), ray.o, inv_of(ray.d), tmin, closest);
+                            h = box_hit_fast(box64(A.tboxes[cur >> 5]), ray.o, inv_of(ray.d), tmin, closest);
                         }
+#ifdef GS_CERT_CHECK
+                        // Diagnostic build: every certified decision re-checked in f64; a
+                        // mismatch is counted (counters[15]) and its first 64 cases recorded
+                        // (item_visits as f64[64][16]: o, d, f64 box, tmin, closest, f32 verdict).
+                        {
+                            const TBox bx = A.tboxes[cur >> 5];
+                            const bool h64 = box_hit(box64(bx), ray.o, inv_of(ray.d), tmin, closest);
+                            if (h64 != h) {
+                                const unsigned long long k = atomicAdd(&P->counters[15], 1ull);
+                                if (k < 64 && P->item_visits) {
+                                    double* rec = reinterpret_cast<double*>(P->item_visits) + k * 16;
+                                    const double v[16] = {ray.o.x, ray.o.y, ray.o.z, ray.d.x, ray.d.y, ray.d.z, bx.mnx,
+                                                          bx.mny, bx.mnz, bx.mxx, bx.mxy, bx.mxz, tmin, closest,
+                                                          (double)h, (double)closest32};
+                                    for (int q = 0; q < 16; q++) rec[q] = v[q];
+                                }
+                            }
+                        }
+#endif
                     } else {  // a wave with a non-cert ray: the f64 compare-select test
-                        h = box_hit(box64(A.tboxes[cur]), ray.o, inv_of(ray.d), tmin, closest);
+                        h = box_hit(box64(A.tboxes[cur >> 5]), ray.o, inv_of(ray.d), tmin, closest);
                     }
                     cur = h ? rb.z : rb.w;
                 }
@@ -1057,8 +1103,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     cur = next;
                 }
             }
-            st = (tracing && cur == THR_END) ? (uint32_t)S_SHADE : st;
         }
+        if (st == S_TRACE && cur == THR_END) st = S_SHADE;
 
         // ---------------------------------------------------------- shade
         GS_STAMP(ts2);
@@ -1638,7 +1684,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             tboxes.resize(nt_rest);
             tleaves.resize(nl_rest);
         }
-        auto tag = [&](uint32_t l) { return l >= n ? THR_END : (thr_leaf[l] ? (THR_LEAF | pos[l]) : pos[l]); };
+        auto tag = [&](uint32_t l) { return l >= n ? THR_END : (thr_leaf[l] ? (THR_LEAF | pos[l]) : pos[l] << 5); };
         for (uint32_t i = 0; i < n; i++) {
             const DNode& r = thr[i];
             if (thr_leaf[i]) {
@@ -1930,7 +1976,9 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
         HIPCHK(hipFuncGetAttributes(&fa, (const void*)kernel_for(ds->feat)));
         int max_lds = 0;
         HIPCHK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
-        const int64_t room = (int64_t)max_lds - (int64_t)fa.sharedSizeBytes - (int64_t)lane_lds_bytes();
+        // The node mirror must start at LDS address 0 (load_tnode): no static LDS.
+        if (fa.sharedSizeBytes != 0) return fail(GS_ERR_UNSUPPORTED, "render kernel with static LDS");
+        const int64_t room = (int64_t)max_lds - (int64_t)lane_lds_bytes();
         if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
         uint32_t ln = ds->lds_nodes, ll = ds->lds_leaves;
         while ((int64_t)ln * (int64_t)sizeof(TNode) + (int64_t)ll * (int64_t)sizeof(TLeaf) > room) {

@@ -20,3 +20,7 @@ find $O/stats -name "*kernel_stats.csv" -exec head -4 {} \;
 if [ "${PMC:-0}" = 1 ]; then
   CONFIG=C4 bash $R/tools/pmc.sh || exit 1
 fi
+if [ "${STAMPS:-0}" = 1 ]; then
+  GS_LIB=$R/grayshift_amd/variants/stamps.so timeout -k 10 200 python3 $R/tools/stamps.py > $O/stamps.txt 2> $O/stamps.err || { echo "stamps failed"; tail -5 $O/stamps.err; exit 1; }
+  cat $O/stamps.txt
+fi
