@@ -1,8 +1,13 @@
+#!/bin/bash
+# Every BASELINE config on one GPU at its stated size and spp, each frame checked against
+# the CPU oracle on a pixel subset sized for ~10 s of CPU work (bench.py's parity block).
+# usage (on the GPU box): bash tools/bench_configs.sh [tag]   -> gpurun_out/<tag>/cfg_<C>.json
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_instancing_noise.py tests/test_gpu_volumes.py -m "gpu and not slow" -x -q --timeout 240 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo "TESTS FAILED"; tail -30 gpurun_out/gpu_tests.log; exit 1; }
-tail -2 gpurun_out/gpu_tests.log
-for c in C1 C2 C3 C4 C5; do
-  timeout -k 10 200 python bench.py --config $c --steps 3 --warmup 1 --no-cpu > gpurun_out/cfg_$c.json 2>gpurun_out/cfg_$c.err || { echo "bench $c failed"; tail -5 gpurun_out/cfg_$c.err; exit 1; }
-  python -c "import json; d=json.loads(open('gpurun_out/cfg_$c.json').read().strip().splitlines()[-1]); print('$c', d['value'], d['ms_per_step'], d['roofline']['frac'])"
+T=${1:-configs}
+O=gpurun_out/$T
+mkdir -p $O
+for spec in "C1 1 3" "C2 4 1" "C3 8 1" "C4 3 3" "C5 24 1"; do
+  set -- $spec
+  timeout -k 10 600 python -u bench.py --config $1 --steps 3 --warmup 1 --cpu-stride $2 --cpu-runs $3 > $O/cfg_$1.json 2> $O/cfg_$1.err || { echo "bench $1 failed"; tail -5 $O/cfg_$1.err; exit 1; }
+  python -c "import json; d=json.loads(open('$O/cfg_$1.json').read().strip().splitlines()[-1]); p=d['parity']; print('$1', d['value'], 'Msamples/s', d['ms_per_step'], 'ms', 'parity max|d| %g over %d px' % (p['max_abs_delta'], p['pixels']), 'cpu', d['cpu_baseline']['value'])"
 done
