@@ -680,6 +680,14 @@ __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull <<
 #define GS_REGION(k, t0) do { } while (0)
 #endif
 
+// ISA census build only (-DGS_ISA_MARKS, tools/isa_census.py): assembler comments that
+// delimit the node pass, its f64 fallback and the leaf pass in the generated code.
+#ifdef GS_ISA_MARKS
+#define GS_MARK(s) asm volatile(";; GS_MARK " s)
+#else
+#define GS_MARK(s) do { } while (0)
+#endif
+
 // Per-lane pixel state lives in LDS ([field][lane], conflict-free), touched once per
 // path; the mirror of the tree's top records follows it.
 enum { L_CSR = 0, L_CSG, L_CSB, L_LSUM, L_LSQ, L_SCOUNT, L_ND };
@@ -1018,6 +1026,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             ln_leaf += leaf_pass ? (uint64_t)__popcll(lm) : 0ull;
 #endif
             if (!leaf_pass) {
+                GS_MARK("node_begin");
                 if (cur < THR_END) {
                     // One 32-B record (2 x 16 B off the SGPR base, offset = cur << 5), the
                     // box test, and the next record: the hit link or the miss link.
@@ -1031,7 +1040,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                                      __uint_as_float(ra.w), __uint_as_float(rb.x), __uint_as_float(rb.y), rc, tmin32,
                                      closest32, undecided);
                         if (undecided) {  // undecided by f32 (rare): the reference's f64 test
+                            GS_MARK("fallback_begin");
                             h = box_hit_fast(box64(A.tboxes[cur >> 5]), ray.o, inv_of(ray.d), tmin, closest);
+                            GS_MARK("fallback_end");
                         }
 #ifdef GS_CERT_CHECK
                         // Diagnostic build: every certified decision re-checked in f64; a
@@ -1053,15 +1064,20 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         }
 #endif
                     } else {  // a wave with a non-cert ray: the f64 compare-select test
+                        GS_MARK("slow_begin");
                         h = box_hit(box64(A.tboxes[cur >> 5]), ray.o, inv_of(ray.d), tmin, closest);
+                        GS_MARK("slow_end");
                     }
                     cur = h ? rb.z : rb.w;
                 }
+                GS_MARK("node_end");
             } else if (at_leaf) {
+                GS_MARK("leaf_begin");
                 double scx, scy, scz, sr;
                 uint32_t next, ref;
                 load_tleaf(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr, next, ref);
                 if ((ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {  // a stationary sphere, inline
+                    GS_MARK("sphere_begin");
                     c_sph++;
                     double t;
                     if (sphere_accept(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
@@ -1070,7 +1086,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         hit_ref = ref;
                         LI(L_HINST) = GS_REF_NONE;
                     }
+                    GS_MARK("sphere_end");
                 } else {
+                    GS_MARK("other_begin");
                     const LeafHit lh = leaf_other<FEAT>(sc, ref, ray, tmin, closest, rng, s_cnt);
                     if (lh.hit) {
                         closest = lh.t;
@@ -1078,6 +1096,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         hit_ref = lh.ref;
                         LI(L_HINST) = lh.inst;
                     }
+                    GS_MARK("other_end");
                 }
                 cur = next;
 #ifndef GS_LEAF_RUN
@@ -1102,6 +1121,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                     cur = next;
                 }
+                GS_MARK("leaf_end");
             }
         }
         if (st == S_TRACE && cur == THR_END) st = S_SHADE;
