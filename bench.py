@@ -51,7 +51,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="C4", help="BASELINE config C1..C5 (default C4)")
+    ap.add_argument("--config", default="C4",
+                    help="BASELINE config C1..C5 (default C4), or a scene name of grayshift_amd.scenes (testing only; "
+                         "not the metric; --width / --spp default to 400 / 64)")
     ap.add_argument("--width", type=int, default=None, help="override (testing only; invalidates the metric)")
     ap.add_argument("--spp", type=int, default=None, help="override (testing only; invalidates the metric)")
     ap.add_argument("--tile", type=int, default=64)
@@ -61,6 +63,7 @@ def parse():
     ap.add_argument("--shade-batch", type=int, default=None)
     ap.add_argument("--blocks-per-cu", type=int, default=None)
     ap.add_argument("--leaf-batch", type=int, default=None)
+    ap.add_argument("--node-steps", type=int, default=0, help="node steps per node pass (0: the scene's choice)")
     ap.add_argument("--sample-chunk", type=int, default=None, help="samples per work item (-1 auto, 0 whole pixel)")
     ap.add_argument("--cpu-stride", type=int, default=3,
                     help="CPU baseline / parity subset at N=1: every Nth row and column")
@@ -113,7 +116,12 @@ def main():
 
     g.set_tuning(a.shade_batch or 52, a.blocks_per_cu or 0, 12 if a.leaf_batch is None else a.leaf_batch,
                  -1 if a.sample_chunk is None else a.sample_chunk)
-    sc = scenes.config(a.config, width=a.width, spp=a.spp)
+    g._native.check(g._native.lib.gs_set_node_steps(a.node_steps))
+    if a.config in scenes.CONFIGS:
+        sc = scenes.config(a.config, width=a.width, spp=a.spp)
+    else:
+        a.width, a.spp = a.width or 400, a.spp or 64
+        sc = scenes.SCENES[a.config](width=a.width, settings=scenes.fixed_spp(a.spp))
     # N > 1: tiles are assigned by a cost-balanced plan (a 1-spp pilot of the frame),
     # computed once at setup on rank 0 and broadcast, so every rank uses the same one
     # (outside the timed region, like the BVH build).
@@ -247,6 +255,7 @@ def main():
                 "seed": a.seed,
                 "rays_per_frame": rays_per_frame, "paths_per_frame": c["paths"],
                 "node_visits_per_ray": round(c["node_visits"] / max(1, rays_per_frame), 3),
+                "scene": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.scene_info().items()},
             },
             "roofline": roofline(a, c, world, kernel_avg_ms, invalid),
             "parity": parity,

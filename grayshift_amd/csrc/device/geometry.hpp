@@ -173,6 +173,13 @@ struct alignas(16) TLeaf {  // 48 B leaf record: a stationary sphere inline, nex
 struct alignas(16) TBox {  // 48 B: the node's f64 box (AABB.rs), for undecided and non-cert rays
     double mnx, mny, mnz, mxx, mxy, mxz;
 };
+// 128 B traversal copy of a quad (the ABI gs_quad, material aside), ordered by use: the
+// plane (normal, D: 32 B) decides most tests; Q, u, v, w (96 B) are read only for a plane
+// hit inside the interval.
+struct alignas(16) TQuad {
+    double nx, ny, nz, d;
+    double qx, qy, qz, ux, uy, uz, vx, vy, vz, wx, wy, wz;
+};
 
 struct RayCert {
     float ix, iy, iz;  // f32(1/d)
@@ -245,20 +252,35 @@ __device__ __forceinline__ bool sphere_accept(d3 c, double r, const Ray& ray, do
     return true;
 }
 
-// Quad::hit acceptance (quad.rs:84-95, plane.rs:20-32).
-__device__ __forceinline__ bool quad_accept(const gs_quad& q, const Ray& ray, double tmin, double tmax, double& t_out) {
-    d3 nrm = ld3(q.normal);
+// Quad::hit acceptance (quad.rs:84-95, plane.rs:20-32), given the plane (normal, D);
+// `tail(Q, u, v, w)` fetches the rest only once the plane hit lies in [tmin, tmax].
+template <class Tail>
+__device__ __forceinline__ bool quad_accept_plane(d3 nrm, double qd, Tail tail, const Ray& ray, double tmin,
+                                                  double tmax, double& t_out) {
     double den = dot(nrm, ray.d);
     if (fabs(den) < 1e-8) return false;
-    double t = (q.d - dot(nrm, ray.o)) / den;
+    double t = (qd - dot(nrm, ray.o)) / den;
     if (!(tmin <= t && t <= tmax)) return false;
+    d3 Q, U, V, W;
+    tail(Q, U, V, W);
     d3 inter = add(ray.o, muls(ray.d, t));
-    d3 planar = sub(inter, ld3(q.q));
-    double alpha = dot(ld3(q.w), cross(planar, ld3(q.v)));
-    double beta = dot(ld3(q.w), cross(ld3(q.u), planar));
+    d3 planar = sub(inter, Q);
+    double alpha = dot(W, cross(planar, V));
+    double beta = dot(W, cross(U, planar));
     if (!(0.0 <= alpha && alpha <= 1.0) || !(0.0 <= beta && beta <= 1.0)) return false;
     t_out = t;
     return true;
+}
+__device__ __forceinline__ bool quad_accept(const gs_quad& q, const Ray& ray, double tmin, double tmax, double& t_out) {
+    return quad_accept_plane(
+        ld3(q.normal), q.d,
+        [&](d3& Q, d3& U, d3& V, d3& W) {
+            Q = ld3(q.q);
+            U = ld3(q.u);
+            V = ld3(q.v);
+            W = ld3(q.w);
+        },
+        ray, tmin, tmax, t_out);
 }
 
 // Triangle::hit (triangle.rs:34-68): one-sided, ray_t ignored (reference quirk).

@@ -141,13 +141,16 @@ struct KArgs {
     const TNode* tnodes;   // the threaded top-level tree: node records (f32 box, links)
     const TLeaf* tleaves;  // its leaf records
     const TBox* tboxes;    // the f64 box of each node record (undecided / non-cert rays)
+    const TQuad* tquads;   // the quads' traversal records (gs_quad order)
     const KParams* P;
     uint32_t root;
     int32_t shade_batch;
     int32_t leaf_batch;  // >= 1: tracing lanes at a leaf before a wave runs a leaf pass
+    int32_t node_steps;  // node steps per node pass, 1 .. GS_NODE_STEPS (per scene, see gs_set_node_steps)
     int32_t cert_boxes;  // every node coordinate |x| <= 1e15: cert rays may take box_cert
     uint32_t lds_nodes;  // node records [0, lds_nodes) are mirrored in each block's LDS,
     uint32_t lds_leaves; // then leaf records [0, lds_leaves)
+    uint32_t lds_quads;  // then quad records [0, lds_quads)
 };
 
 enum { S_NEED = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };
@@ -241,6 +244,100 @@ __device__ __forceinline__ void load_tleaf(const uint8_t* s_leaves, const TLeaf*
     ref = d.y;
 }
 
+// Quad records for traversal (TQuad): [0, n_lds) from the block's LDS mirror, the rest
+// from global memory; 16 B at a time, so a quad whose plane misses reads 32 B, not 128.
+struct QuadSrc {
+    const uint8_t* lds;
+    const TQuad* g;
+    uint32_t n_lds;
+};
+
+// Scene-record loads of the leaf tests, field by field through a pointer of an explicit
+// address space: global (vector loads) or, with UNI — every active lane tests the same
+// leaf, a wave-uniform ref — constant, which compiles to scalar loads (the scalar cache:
+// no vector-memory instruction, no per-lane address, uniform branches after them).  The
+// scene's pointers are generic and load through flat instructions otherwise (which also
+// count against lgkmcnt); a whole-struct copy from constant memory is rewritten by the
+// optimiser into flat loads again, hence the field-wise copies.
+#ifdef __HIP_DEVICE_COMPILE__
+#define GS_SCENE_AS(UNI) __attribute__((address_space((UNI) ? 4 : 1)))
+#else
+#define GS_SCENE_AS(UNI)
+#endif
+template <bool UNI, class T>
+__device__ __forceinline__ const GS_SCENE_AS(UNI) T* sp(const T* p) {
+    return (const GS_SCENE_AS(UNI) T*)p;
+}
+template <bool UNI>
+__device__ __forceinline__ uint32_t ld_u32(const uint32_t* p) {
+    return *sp<UNI>(p);
+}
+template <bool UNI>
+__device__ __forceinline__ gs_instance ld_inst(const gs_instance* p) {
+    const auto q = sp<UNI>(p);
+    gs_instance v;
+    v.kind = q->kind;
+    v.child = q->child;
+    v.p[0] = q->p[0];
+    v.p[1] = q->p[1];
+    v.p[2] = q->p[2];
+    return v;
+}
+template <bool UNI>
+__device__ __forceinline__ gs_list ld_list(const gs_list* p) {
+    const auto q = sp<UNI>(p);
+    gs_list v;
+    v.first = q->first;
+    v.count = q->count;
+    return v;
+}
+template <bool UNI>
+__device__ __forceinline__ gs_medium ld_medium(const gs_medium* p) {
+    const auto q = sp<UNI>(p);
+    gs_medium v;
+    v.boundary = q->boundary;
+    v.material = q->material;
+    v.density_neg_inv = q->density_neg_inv;
+    return v;
+}
+__device__ __forceinline__ DNode ld_node_g(const DNode* p) {  // a nested-BVH node (global loads)
+    const auto q = sp<false>(reinterpret_cast<const u32x4*>(p));
+    const u32x4 a = q[0], b = q[1], c = q[2], d = q[3];
+    DNode n;
+    n.mnx = lo_hi(a.x, a.y);
+    n.mny = lo_hi(a.z, a.w);
+    n.mnz = lo_hi(b.x, b.y);
+    n.mxx = lo_hi(b.z, b.w);
+    n.mxy = lo_hi(c.x, c.y);
+    n.mxz = lo_hi(c.z, c.w);
+    n.left = d.x;
+    n.right = d.y;
+    n.pad0 = d.z;
+    n.pad1 = d.w;
+    return n;
+}
+template <bool UNI>
+__device__ __forceinline__ u32x4 quad_part(const QuadSrc& qs, uint32_t i, uint32_t k) {
+    if (!UNI && i < qs.n_lds) return ((lds_u32x4*)(qs.lds + i * (uint32_t)sizeof(TQuad)))[k];
+    return sp<UNI>(reinterpret_cast<const u32x4*>(qs.g + i))[k];
+}
+template <bool UNI>
+__device__ __forceinline__ bool quad_test(const QuadSrc& qs, uint32_t i, const Ray& ray, double tmin, double tmax,
+                                          double& t_out) {
+    const u32x4 a = quad_part<UNI>(qs, i, 0), b = quad_part<UNI>(qs, i, 1);
+    return quad_accept_plane(
+        mk(lo_hi(a.x, a.y), lo_hi(a.z, a.w), lo_hi(b.x, b.y)), lo_hi(b.z, b.w),
+        [&](d3& Q, d3& U, d3& V, d3& W) {
+            const u32x4 c = quad_part<UNI>(qs, i, 2), e = quad_part<UNI>(qs, i, 3), f = quad_part<UNI>(qs, i, 4);
+            const u32x4 g = quad_part<UNI>(qs, i, 5), h = quad_part<UNI>(qs, i, 6), m = quad_part<UNI>(qs, i, 7);
+            Q = mk(lo_hi(c.x, c.y), lo_hi(c.z, c.w), lo_hi(e.x, e.y));
+            U = mk(lo_hi(e.z, e.w), lo_hi(f.x, f.y), lo_hi(f.z, f.w));
+            V = mk(lo_hi(g.x, g.y), lo_hi(g.z, g.w), lo_hi(h.x, h.y));
+            W = mk(lo_hi(h.z, h.w), lo_hi(m.x, m.y), lo_hi(m.z, m.w));
+        },
+        ray, tmin, tmax, t_out);
+}
+
 // Outcome of testing one non-node child against the ray.
 struct LeafHit {
     bool hit;
@@ -250,28 +347,38 @@ struct LeafHit {
 
 // One primitive ref against `ray` (already in the primitive's space); accepts into
 // `res` ("last accepted wins", as BVH.rs:73-80 and hittable.rs:75-83 compose).
-__device__ __forceinline__ void prim_test(const DevScene& sc, uint32_t ref, const Ray& ray, double tmin,
-                                          double closest, uint32_t inst_ref, LeafHit& res,
+template <bool UNI>
+__device__ __forceinline__ void prim_test(const DevScene& sc, const QuadSrc& qs, uint32_t ref, const Ray& ray,
+                                          double tmin, double closest, uint32_t inst_ref, LeafHit& res,
                                           unsigned long long* cnt) {
     const uint32_t kind = ref >> GS_REF_SHIFT, idx = ref & GS_REF_MASK;
     double t;
     bool ok = false;
     if (kind == GS_REF_SPHERE) {
         atomicAdd(&cnt[C_SPH], 1ull);
-        DSphere s = sc.spheres[idx];
-        ok = sphere_accept(mk(s.cx, s.cy, s.cz), s.r, ray, len2(ray.d), tmin, closest, t);
+        const auto s = sp<UNI>(sc.spheres + idx);
+        ok = sphere_accept(mk(s->cx, s->cy, s->cz), s->r, ray, len2(ray.d), tmin, closest, t);
     } else if (kind == GS_REF_MSPHERE) {
         atomicAdd(&cnt[C_MSPH], 1ull);
-        const gs_msphere& s = sc.mspheres[idx];
-        d3 c = add(ld3(s.center_start), muls(ld3(s.center_path), ray.time));
-        ok = sphere_accept(c, s.radius, ray, len2(ray.d), tmin, closest, t);
+        const auto s = sp<UNI>(sc.mspheres + idx);
+        const d3 c0 = mk(s->center_start[0], s->center_start[1], s->center_start[2]);
+        const d3 cp = mk(s->center_path[0], s->center_path[1], s->center_path[2]);
+        d3 c = add(c0, muls(cp, ray.time));
+        ok = sphere_accept(c, s->radius, ray, len2(ray.d), tmin, closest, t);
     } else if (kind == GS_REF_QUAD) {
         atomicAdd(&cnt[C_QUAD], 1ull);
-        ok = quad_accept(sc.quads[idx], ray, tmin, closest, t);
+        ok = quad_test<UNI>(qs, idx, ray, tmin, closest, t);
     } else if (kind == GS_REF_TRIANGLE) {
         atomicAdd(&cnt[C_TRI], 1ull);
         double u, v;
-        ok = tri_hit(sc.tris[idx], ray, t, u, v);
+        const auto q = sp<UNI>(sc.tris + idx);
+        gs_triangle tr;
+        for (int k = 0; k < 3; k++) {
+            tr.a[k] = q->a[k];
+            tr.b[k] = q->b[k];
+            tr.c[k] = q->c[k];
+        }
+        ok = tri_hit(tr, ray, t, u, v);
     }
     if (ok) {
         res.hit = true;
@@ -283,10 +390,11 @@ __device__ __forceinline__ void prim_test(const DevScene& sc, uint32_t ref, cons
 
 // Translate / RotateY chain (hittable.rs:107-113, :179-193): the ray in the innermost
 // child's space; returns that child's ref.
+template <bool UNI>
 __device__ __forceinline__ uint32_t walk_chain(const DevScene& sc, uint32_t cur, Ray& r, unsigned long long* cnt) {
 #pragma unroll 1
     for (int k = 0; k < GS_MAX_CHAIN && (cur >> GS_REF_SHIFT) == GS_REF_INSTANCE; k++) {
-        const gs_instance& in = sc.inst[cur & GS_REF_MASK];
+        const gs_instance in = ld_inst<UNI>(sc.inst + (cur & GS_REF_MASK));
         atomicAdd(&cnt[C_INST], 1ull);
         inst_forward(in, r);
         cur = in.child;
@@ -295,41 +403,44 @@ __device__ __forceinline__ uint32_t walk_chain(const DevScene& sc, uint32_t cur,
 }
 
 // A HittableList (hittable.rs:71-86: shrinking closest) or one primitive.
-__device__ __forceinline__ void shape_test(const DevScene& sc, uint32_t cur, const Ray& r, double tmin, double closest,
-                                           uint32_t inst_ref, LeafHit& res, unsigned long long* cnt) {
+template <bool UNI>
+__device__ __forceinline__ void shape_test(const DevScene& sc, const QuadSrc& qs, uint32_t cur, const Ray& r,
+                                           double tmin, double closest, uint32_t inst_ref, LeafHit& res,
+                                           unsigned long long* cnt) {
     if ((cur >> GS_REF_SHIFT) == GS_REF_LIST) {
         atomicAdd(&cnt[C_LIST], 1ull);
-        const gs_list l = sc.lists[cur & GS_REF_MASK];
+        const gs_list l = ld_list<UNI>(sc.lists + (cur & GS_REF_MASK));
 #pragma unroll 1
         for (uint32_t k = 0; k < l.count; k++)
-            prim_test(sc, sc.list_refs[l.first + k], r, tmin, res.t, inst_ref, res, cnt);
+            prim_test<UNI>(sc, qs, ld_u32<UNI>(sc.list_refs + l.first + k), r, tmin, res.t, inst_ref, res, cnt);
     } else {
-        prim_test(sc, cur, r, tmin, closest, inst_ref, res, cnt);
+        prim_test<UNI>(sc, qs, cur, r, tmin, closest, inst_ref, res, cnt);
     }
 }
 
 // ConstantMedium::hit (volume.rs:32-63): the boundary hit over Interval::UNIVERSE, again
 // from t1 + 0.0001, both clipped to ray_t; then the free-flight distance from the lane's
 // RNG stream, drawn here, inside traversal, in the reference's visit order (:48).
-__device__ __forceinline__ void medium_test(const DevScene& sc, uint32_t cur, const Ray& r, double tmin,
+template <bool UNI>
+__device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& qs, uint32_t cur, const Ray& r, double tmin,
                                             double closest, uint32_t inst_ref, uint64_t& rng, LeafHit& res,
                                             unsigned long long* cnt) {
     atomicAdd(&cnt[C_MED], 1ull);
-    const gs_medium md = sc.media[cur & GS_REF_MASK];
+    const gs_medium md = ld_medium<UNI>(sc.media + (cur & GS_REF_MASK));
     const double DMAX = 1.7976931348623157e308;  // f64::MAX; f64::MIN = -f64::MAX
     LeafHit b1;
     b1.hit = false;
     b1.t = DMAX;
     Ray rb = r;
-    const uint32_t shape = walk_chain(sc, md.boundary, rb, cnt);
-    shape_test(sc, shape, rb, -DMAX, DMAX, GS_REF_NONE, b1, cnt);
+    const uint32_t shape = walk_chain<UNI>(sc, md.boundary, rb, cnt);
+    shape_test<UNI>(sc, qs, shape, rb, -DMAX, DMAX, GS_REF_NONE, b1, cnt);
     if (!b1.hit) return;
     LeafHit b2;
     b2.hit = false;
     b2.t = DMAX;
     rb = r;
-    walk_chain(sc, md.boundary, rb, cnt);  // the second boundary.hit call walks the chain again
-    shape_test(sc, shape, rb, b1.t + 0.0001, DMAX, GS_REF_NONE, b2, cnt);
+    walk_chain<UNI>(sc, md.boundary, rb, cnt);  // the second boundary.hit call walks the chain again
+    shape_test<UNI>(sc, qs, shape, rb, b1.t + 0.0001, DMAX, GS_REF_NONE, b2, cnt);
     if (!b2.hit) return;
     double t1 = b1.t, t2 = b2.t;
     if (t1 < tmin) t1 = tmin;
@@ -350,7 +461,7 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, uint32_t cur, co
 // 741-755): BVHNode::hit (BVH.rs:69-90) on the ray in the instance's space, as the same
 // left-first walk with a shrinking closest t as the top level, on a private stack.
 // `root`: a device node ref.  Leaves are lists or primitives (validated on the host).
-__device__ __forceinline__ void nested_bvh(const DevScene& sc, uint32_t root, const Ray& r, double tmin,
+__device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs, uint32_t root, const Ray& r, double tmin,
                                            double closest, uint32_t inst_ref, LeafHit& res,
                                            unsigned long long* cnt) {
     // AABB::hit's `1.0 / ray.direction[axis]` (AABB.rs:64), hoisted per ray (same value)
@@ -366,7 +477,7 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, uint32_t root, co
         }
         if (cur < DREF_LEAF) {
             atomicAdd(&cnt[C_NODES], 1ull);
-            const DNode n = load_node(sc.nodes + cur);
+            const DNode n = ld_node_g(sc.nodes + cur);
             if (box_hit_v(n, r.o, inv, tmin, closest)) {
                 if (n.right != DREF_NONE) stk[sp++] = n.right;
                 cur = n.left;
@@ -374,7 +485,7 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, uint32_t root, co
                 cur = DREF_NONE;
             }
         } else {
-            shape_test(sc, cur, r, tmin, closest, inst_ref, res, cnt);
+            shape_test<false>(sc, qs, cur, r, tmin, closest, inst_ref, res, cnt);
             if (res.hit) closest = res.t;  // res.t only ever shrinks
             cur = DREF_NONE;
         }
@@ -387,22 +498,22 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, uint32_t root, co
 // from the lane's stream.  FEAT (GS_FEAT_*) is a kernel template argument: scenes
 // without media / nested BVHs compile those out (the medium test costs the traversal
 // loop 4 VGPRs and spills otherwise; the nested walk uses private memory).
-template <int FEAT>
-__device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, uint32_t ref, Ray r, double tmin, double closest,
-                                           uint64_t& rng, unsigned long long* cnt) {
+template <int FEAT, bool UNI>
+__device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, const QuadSrc& qs, uint32_t ref, Ray r, double tmin,
+                                           double closest, uint64_t& rng, unsigned long long* cnt) {
     LeafHit res;
     res.hit = false;
     res.t = closest;
     res.ref = GS_REF_NONE;
     res.inst = GS_REF_NONE;
     const uint32_t inst_ref = (ref >> GS_REF_SHIFT) == GS_REF_INSTANCE ? ref : GS_REF_NONE;
-    const uint32_t cur = walk_chain(sc, ref, r, cnt);
+    const uint32_t cur = walk_chain<UNI>(sc, ref, r, cnt);
     if ((FEAT & GS_FEAT_MEDIA) && (cur >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
-        medium_test(sc, cur, r, tmin, closest, inst_ref, rng, res, cnt);
+        medium_test<UNI>(sc, qs, cur, r, tmin, closest, inst_ref, rng, res, cnt);
     } else if ((FEAT & GS_FEAT_NESTED) && (cur >> GS_REF_SHIFT) == GS_REF_NODE) {
-        nested_bvh(sc, cur & GS_REF_MASK, r, tmin, closest, inst_ref, res, cnt);
+        nested_bvh(sc, qs, cur & GS_REF_MASK, r, tmin, closest, inst_ref, res, cnt);
     } else {
-        shape_test(sc, cur, r, tmin, closest, inst_ref, res, cnt);
+        shape_test<UNI>(sc, qs, cur, r, tmin, closest, inst_ref, res, cnt);
     }
     return res;
 }
@@ -718,6 +829,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     // a node's LDS address is cur << 5 plus a constant the ds_read offset absorbs.
     uint8_t* s_nodes = smem;
     uint8_t* s_leaves = s_nodes + (size_t)A.lds_nodes * sizeof(TNode);
+    uint8_t* s_quads = s_leaves + (size_t)A.lds_leaves * sizeof(TLeaf);
     {
         const uint4* src = reinterpret_cast<const uint4*>(A.tnodes);
         uint4* dst = reinterpret_cast<uint4*>(s_nodes);
@@ -725,9 +837,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         src = reinterpret_cast<const uint4*>(A.tleaves);
         dst = reinterpret_cast<uint4*>(s_leaves);
         for (uint32_t k = threadIdx.x; k < A.lds_leaves * 3u; k += GS_BLOCK) dst[k] = src[k];
+        src = reinterpret_cast<const uint4*>(A.tquads);
+        dst = reinterpret_cast<uint4*>(s_quads);
+        for (uint32_t k = threadIdx.x; k < A.lds_quads * 8u; k += GS_BLOCK) dst[k] = src[k];
     }
+    const QuadSrc qs{s_quads, A.tquads, A.lds_quads};
     // Per-lane pixel / path state after the mirror: [L_ND][GS_BLOCK] f64, [L_NI][GS_BLOCK] u32.
-    double* s_d = (double*)(s_leaves + (size_t)A.lds_leaves * sizeof(TLeaf));
+    double* s_d = (double*)(s_quads + (size_t)A.lds_quads * sizeof(TQuad));
     uint32_t* s_i = (uint32_t*)(s_d + L_ND * GS_BLOCK);
     unsigned long long* s_cnt = (unsigned long long*)(s_i + L_NI * GS_BLOCK);
 #ifdef GS_STAMPS
@@ -891,6 +1007,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     };
 
     uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, acc_refill = 0, acc_trav = 0, acc_shade = 0;
+    uint64_t acc_node = 0, acc_leaf = 0;  // stamps build: wave clock in node / leaf passes
+    uint64_t dist_ref = 0, dist_kind = 0;  // stamps build: distinct leaf refs / ref kinds per leaf pass
     uint64_t it_all = 0, it_node = 0, it_leaf = 0, ln_node = 0, ln_leaf = 0, it_shade = 0, ln_shade = 0;
 #pragma unroll 1
     for (;;) {
@@ -1019,6 +1137,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             const uint64_t lm = __builtin_amdgcn_ballot_w64(at_leaf);
             const bool leaf_pass = lm == tr || (uint32_t)__popcll(lm) >= (uint32_t)A.leaf_batch;
 #ifdef GS_STAMPS
+            uint64_t tp0;
+            GS_STAMP(tp0);
             it_all++;
             it_node += !leaf_pass;
             it_leaf += leaf_pass;
@@ -1027,6 +1147,24 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #endif
             if (!leaf_pass) {
                 GS_MARK("node_begin");
+// A node pass takes up to GS_NODE_STEPS node steps per lane, unrolled (the loop head's
+// ballots, shade-count and pass-kind tests are paid once per pass, not per node):
+// measured on MI355X C4 (leaf batch 12), Msamples/s: 1 step 5487, 2 5788, 4 6049, 8 6205;
+// unrolled 4 6303, 6 6384, 8 6451-6456, 10 6417, 12 6334, 16 6378; a ballot to leave the
+// pass early once no lane is at a node cost 6% (8 steps: 5833).
+#ifndef GS_NODE_STEPS
+#define GS_NODE_STEPS 8
+#endif
+#ifndef GS_NODE_UNROLL
+#define GS_NODE_UNROLL GS_NODE_STEPS
+#endif
+                constexpr int kNodeUnroll = GS_NODE_UNROLL;  // (a macro in the pragma breaks --save-temps)
+#pragma unroll kNodeUnroll
+                for (int nstep = 0; nstep < GS_NODE_STEPS; nstep++) {
+                if (nstep >= A.node_steps) break;  // wave-uniform (an SGPR compare)
+#ifdef GS_NODE_STEPS_EXIT
+                if (nstep > 0 && __builtin_amdgcn_ballot_w64(cur < THR_END) == 0) break;
+#endif
                 if (cur < THR_END) {
                     // One 32-B record (2 x 16 B off the SGPR base, offset = cur << 5), the
                     // box test, and the next record: the hit link or the miss link.
@@ -1070,12 +1208,31 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                     cur = h ? rb.z : rb.w;
                 }
+                }
                 GS_MARK("node_end");
             } else if (at_leaf) {
                 GS_MARK("leaf_begin");
                 double scx, scy, scz, sr;
                 uint32_t next, ref;
                 load_tleaf(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr, next, ref);
+#ifdef GS_STAMPS
+                {  // counted by the pass's first active lane (summed over lanes at the end)
+                    const uint64_t act = __builtin_amdgcn_ballot_w64(true);
+                    const bool first = __builtin_ctzll(act) == (uint32_t)lane;
+                    uint64_t m = act;
+                    while (m) {
+                        const uint32_t r0 = __builtin_amdgcn_readlane(ref, __builtin_ctzll(m));
+                        m &= ~__builtin_amdgcn_ballot_w64(ref == r0);
+                        dist_ref += first;
+                    }
+                    m = act;
+                    while (m) {
+                        const uint32_t k0 = __builtin_amdgcn_readlane(ref, __builtin_ctzll(m)) >> GS_REF_SHIFT;
+                        m &= ~__builtin_amdgcn_ballot_w64((ref >> GS_REF_SHIFT) == k0);
+                        dist_kind += first;
+                    }
+                }
+#endif
                 if ((ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {  // a stationary sphere, inline
                     GS_MARK("sphere_begin");
                     c_sph++;
@@ -1089,7 +1246,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     GS_MARK("sphere_end");
                 } else {
                     GS_MARK("other_begin");
-                    const LeafHit lh = leaf_other<FEAT>(sc, ref, ray, tmin, closest, rng, s_cnt);
+                    // A leaf pass whose other-kind lanes all sit at one leaf (the Cornell box:
+                    // always, with single node steps) tests it with scalar loads.
+                    const uint32_t r0 = __builtin_amdgcn_readfirstlane(ref);
+                    const bool uni = __builtin_amdgcn_ballot_w64(ref != r0) == 0;
+                    LeafHit lh;
+                    if (uni) lh = leaf_other<FEAT, true>(sc, qs, r0, ray, tmin, closest, rng, s_cnt);
+                    else lh = leaf_other<FEAT, false>(sc, qs, ref, ray, tmin, closest, rng, s_cnt);
                     if (lh.hit) {
                         closest = lh.t;
                         closest32 = (float)lh.t;
@@ -1123,6 +1286,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 }
                 GS_MARK("leaf_end");
             }
+#ifdef GS_STAMPS
+            {
+                uint64_t tp1;
+                GS_STAMP(tp1);
+                (leaf_pass ? acc_leaf : acc_node) += tp1 - tp0;
+            }
+#endif
         }
         if (st == S_TRACE && cur == THR_END) st = S_SHADE;
 
@@ -1195,6 +1365,11 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #endif
     }
 #ifdef GS_STAMPS
+    if (P->item_visits && (dist_ref || dist_kind)) {
+        unsigned long long* dbg = (unsigned long long*)P->item_visits;
+        atomicAdd(&dbg[17], (unsigned long long)dist_ref);
+        atomicAdd(&dbg[18], (unsigned long long)dist_kind);
+    }
     if (lane == 0 && P->item_visits) {
         unsigned long long* dbg = (unsigned long long*)P->item_visits;
         atomicAdd(&dbg[0], (unsigned long long)acc_refill);
@@ -1208,6 +1383,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         atomicAdd(&dbg[8], (unsigned long long)it_shade);
         atomicAdd(&dbg[9], (unsigned long long)ln_shade);
         for (int k = 0; k < 5; k++) atomicAdd(&dbg[10 + k], s_reg[(tid >> 6) * 8 + k]);
+        atomicAdd(&dbg[15], (unsigned long long)acc_node);
+        atomicAdd(&dbg[16], (unsigned long long)acc_leaf);
+
     }
 #endif
 #undef LD
@@ -1281,6 +1459,7 @@ __global__ void gs_combine_kernel(const KParams* __restrict__ P) {
 static thread_local std::string tl_err;
 static int32_t g_shade_batch = 52;  // swept on MI355X C4 (chunked, uniform loop): 48 -> 3502, 52 -> 3535-3568, 56 -> 3506-3536 Msamples/s
 static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
+static int32_t g_node_steps = 0;  // 0: the scene's own (gs_device_scene.node_steps)
 static int32_t g_leaf_batch = 12;  // swept on MI355X C4 with leaf runs: 8 -> 4586, 10 -> 4632, 12 -> 4648-4651, 14 -> 4624, 16 -> 4592
 // Bytes of threaded records mirrored in LDS per block (the most-tested ones): what is
 // left of the block's share of the CU's 160 KiB (4 waves/SIMD = 1024 lanes per CU) after
@@ -1339,14 +1518,18 @@ struct gs_device_scene {
     const TNode* tnodes = nullptr;
     const TBox* tboxes = nullptr;
     const TLeaf* tleaves = nullptr;
+    const TQuad* tquads = nullptr;  // every quad's traversal record, gs_quad order
     uint32_t thr_root = THR_END;
-    uint32_t lds_nodes = 0, lds_leaves = 0;  // mirrored prefixes (per block)
+    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0;  // mirrored prefixes (per block)
+    int32_t node_steps = GS_NODE_STEPS;      // node steps per node pass (from the tree's shape)
+    uint32_t node_records = 0, leaf_records = 0;
+    double nodes_per_leaf = 0.0, other_leaf_frac = 0.0;
     // Launch state, mutated by launches of a const scene: guarded by `mu`.
     std::mutex mu;
     // launch geometry, computed at the first launch (host API queries cost ~0.5 ms each)
     bool launch_ready = false;
     int cus = 0, per_cu = 0;
-    uint32_t launch_lds_nodes = 0, launch_lds_leaves = 0;
+    uint32_t launch_lds_nodes = 0, launch_lds_leaves = 0, launch_lds_quads = 0;
     size_t launch_lds = 0;
     LaunchSlot slots[kLaunchSlots];
     uint32_t next_slot = 0;
@@ -1568,6 +1751,12 @@ extern "C" {
 const char* gs_last_error(void) { return tl_err.c_str(); }
 int32_t gs_version(void) { return GS_ABI_VERSION; }
 
+gs_status gs_set_node_steps(int32_t node_steps) {
+    if (node_steps < 0 || node_steps > GS_NODE_STEPS) return fail(GS_ERR_ARG, "node_steps outside [0, GS_NODE_STEPS]");
+    g_node_steps = node_steps;
+    return GS_OK;
+}
+
 gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf_batch, int32_t sample_chunk) {
     if (shade_batch < 1 || shade_batch > 64 || blocks_per_cu < 0 || blocks_per_cu > 8 || leaf_batch < 0 ||
         leaf_batch > 64 || sample_chunk < -1)
@@ -1607,8 +1796,10 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     std::vector<TNode> tnodes;
     std::vector<TBox> tboxes;
     std::vector<TLeaf> tleaves;
-    uint32_t lds_nodes = 0, lds_leaves = 0, thr_root_tagged = THR_END;
+    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, thr_root_tagged = THR_END;
+    double nodes_per_leaf = 0.0, other_leaf_frac = 0.0;
     bool leaf_runs = false;
+    int32_t auto_node_steps = GS_NODE_STEPS;
     {
         // Iterative pre-order: a node pushes a "close" marker below its children, which
         // sets its miss link once its subtree is emitted.
@@ -1680,12 +1871,33 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
                 return score[a] > score[b] || (score[a] == score[b] && depth[a] < depth[b]);
             });
+            // Expected node tests per leaf test (the score over the root box's area is the
+            // chance a ray entering the root tests the record).
+            if (n && !thr_leaf[0]) {
+                const DNode& b = thr[0];
+                const double dx = b.mxx - b.mnx, dy = b.mxy - b.mny, dz = b.mxz - b.mnz;
+                const double sa_root = dx * dy + dy * dz + dz * dx;
+                double pn = 0.0, pl = 0.0, po = 0.0;
+                for (uint32_t i = 0; i < n; i++) {
+                    const double p = i == 0 ? 1.0 : (sa_root > 0.0 ? std::min(1.0, score[i] / sa_root) : 1.0);
+                    (thr_leaf[i] ? pl : pn) += p;
+                    if (thr_leaf[i] && (thr[i].right >> GS_REF_SHIFT) != GS_REF_SPHERE) po += p;
+                }
+                nodes_per_leaf = pl > 0.0 ? pn / pl : 0.0;
+                other_leaf_frac = pl > 0.0 ? po / pl : 0.0;
+            } else if (n) {
+                other_leaf_frac = (thr[0].right >> GS_REF_SHIFT) != GS_REF_SPHERE ? 1.0 : 0.0;
+            }
             // Fill the LDS byte budget in that order (32-B node records, 48-B leaf records).
             const int64_t budget = g_lds_mirror < 0 ? lds_mirror_budget() : g_lds_mirror;
             std::vector<uint8_t> top(n, 0);
             int64_t used = 0;
+#ifndef GS_LDS_LEAVES
+#define GS_LDS_LEAVES 1  // 0: mirror node records only
+#endif
             for (uint32_t i = 0; i < n; i++) {
                 const uint32_t r = order[i];
+                if (!GS_LDS_LEAVES && thr_leaf[r]) continue;
                 const int64_t sz = thr_leaf[r] ? (int64_t)sizeof(TLeaf) : (int64_t)sizeof(TNode);
                 if (used + sz > budget) {
                     if (used + (int64_t)sizeof(TNode) > budget) break;
@@ -1695,6 +1907,9 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                 top[r] = 1;
                 (thr_leaf[r] ? lds_leaves : lds_nodes)++;
             }
+            // Quads (a prefix in gs_quad order) take what the tree leaves of the budget.
+            lds_quads = (uint32_t)std::min<int64_t>(s->n_quads,
+                                                    std::max<int64_t>(0, budget - used) / (int64_t)sizeof(TQuad));
             uint32_t nt = 0, nl = 0, nt_rest = lds_nodes, nl_rest = lds_leaves;
             for (uint32_t i = 0; i < n; i++) {
                 if (thr_leaf[i]) pos[i] = top[i] ? nl++ : nl_rest++;
@@ -1727,6 +1942,12 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                 pairs += i + 1 < n && is_sph(i) && is_sph(i + 1);
             }
             leaf_runs = leaves && pairs * 4 >= leaves;
+            // Node steps per node pass (MI355X, Msamples/s).  Sphere-only trees take long
+            // node runs (C4: 3 -> 6101, 8 -> 6347).  Trees whose leaf tests are mostly other
+            // kinds keep their lanes in step, one node per pass, so that a leaf pass finds
+            // them at one leaf and takes the scalar-load path (C3: 1 -> 10336, 3 -> 9194,
+            // 8 -> 6818).  Mixed trees in between (C5: 3 -> 5629, 8 -> 5088).
+            auto_node_steps = other_leaf_frac == 0.0 ? GS_NODE_STEPS : (other_leaf_frac >= 0.5 ? 1 : 3);
         }
     }
     if (tnodes.size() >= (1u << 26) || tleaves.size() >= (1u << 26))
@@ -1735,6 +1956,12 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     for (const TBox& b : tboxes)
         for (double v : {b.mnx, b.mny, b.mnz, b.mxx, b.mxy, b.mxz})
             if (!(std::fabs(v) <= 1e15)) cert_boxes = false;
+    std::vector<TQuad> tquads(s->n_quads);
+    for (uint32_t i = 0; i < s->n_quads; i++) {
+        const gs_quad& q = s->quads[i];
+        tquads[i] = TQuad{q.normal[0], q.normal[1], q.normal[2], q.d, q.q[0], q.q[1], q.q[2], q.u[0],
+                          q.u[1],      q.u[2],      q.v[0],      q.v[1], q.v[2], q.w[0], q.w[1], q.w[2]};
+    }
     std::vector<DSphere> sph(s->n_spheres);
     std::vector<uint32_t> sph_mat(s->n_spheres);
     for (uint32_t i = 0; i < s->n_spheres; i++) {
@@ -1793,6 +2020,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     size_t o_tnodes = L.add(tnodes.data(), tnodes.size() * sizeof(TNode));
     size_t o_tboxes = L.add(tboxes.data(), tboxes.size() * sizeof(TBox));
     size_t o_tleaves = L.add(tleaves.data(), tleaves.size() * sizeof(TLeaf));
+    size_t o_tquads = L.add(tquads.data(), tquads.size() * sizeof(TQuad));
     size_t o_sph = L.add(sph.data(), sph.size() * sizeof(DSphere));
     size_t o_sphm = L.add(sph_mat.data(), sph_mat.size() * 4);
     size_t o_msph = L.add(s->mspheres, s->n_mspheres * sizeof(gs_msphere));
@@ -1858,13 +2086,37 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ds->tnodes = (const TNode*)(b + o_tnodes);
     ds->tboxes = (const TBox*)(b + o_tboxes);
     ds->tleaves = (const TLeaf*)(b + o_tleaves);
+    ds->tquads = (const TQuad*)(b + o_tquads);
     ds->thr_root = thr_root_tagged;
     ds->lds_nodes = lds_nodes;
     ds->lds_leaves = lds_leaves;
+    ds->lds_quads = lds_quads;
+    ds->node_records = (uint32_t)tnodes.size();
+    ds->leaf_records = (uint32_t)tleaves.size();
+    ds->nodes_per_leaf = nodes_per_leaf;
+    ds->other_leaf_frac = other_leaf_frac;
     ds->bvh_depth = depth < 1 ? 1 : depth;
     ds->feat = (s->n_media != 0 ? GS_FEAT_MEDIA : 0) | (nested ? GS_FEAT_NESTED : 0) | (leaf_runs ? GS_FEAT_LEAFRUN : 0);
     ds->cert_boxes = cert_boxes;
+    ds->node_steps = auto_node_steps;
     *out = ds;
+    return GS_OK;
+}
+
+gs_status gs_device_scene_info(const gs_device_scene* ds, gs_scene_info* out) {
+    if (!ds || !out) return fail(GS_ERR_ARG, "null argument");
+    gs_scene_info i{};
+    i.node_records = ds->node_records;
+    i.leaf_records = ds->leaf_records;
+    i.lds_nodes = ds->lds_nodes;
+    i.lds_leaves = ds->lds_leaves;
+    i.lds_quads = ds->lds_quads;
+    i.feat = ds->feat;
+    i.node_steps = std::max(1, std::min<int32_t>(GS_NODE_STEPS, g_node_steps > 0 ? g_node_steps : ds->node_steps));
+    i.cert_boxes = ds->cert_boxes ? 1 : 0;
+    i.nodes_per_leaf = ds->nodes_per_leaf;
+    i.other_leaf_frac = ds->other_leaf_frac;
+    *out = i;
     return GS_OK;
 }
 
@@ -1982,10 +2234,12 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     a.tnodes = ds->tnodes;
     a.tboxes = ds->tboxes;
     a.tleaves = ds->tleaves;
+    a.tquads = ds->tquads;
     a.root = ds->thr_root;
     a.cert_boxes = ds->cert_boxes ? 1 : 0;
     a.shade_batch = g_shade_batch;
     a.leaf_batch = g_leaf_batch < 1 ? 1 : g_leaf_batch;  // 0 would never step a node
+    a.node_steps = std::max(1, std::min<int32_t>(GS_NODE_STEPS, g_node_steps > 0 ? g_node_steps : ds->node_steps));
     gs_device_scene* mds = const_cast<gs_device_scene*>(ds);
     std::lock_guard<std::mutex> lock(mds->mu);
     if (!mds->launch_ready) {
@@ -2000,14 +2254,20 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
         if (fa.sharedSizeBytes != 0) return fail(GS_ERR_UNSUPPORTED, "render kernel with static LDS");
         const int64_t room = (int64_t)max_lds - (int64_t)lane_lds_bytes();
         if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
-        uint32_t ln = ds->lds_nodes, ll = ds->lds_leaves;
-        while ((int64_t)ln * (int64_t)sizeof(TNode) + (int64_t)ll * (int64_t)sizeof(TLeaf) > room) {
-            if (ln) ln = ln - 1 - ln / 16;  // shrink both prefixes until they fit
+        uint32_t ln = ds->lds_nodes, ll = ds->lds_leaves, lq = ds->lds_quads;
+        auto bytes = [&] {
+            return (int64_t)ln * (int64_t)sizeof(TNode) + (int64_t)ll * (int64_t)sizeof(TLeaf) +
+                   (int64_t)lq * (int64_t)sizeof(TQuad);
+        };
+        while (bytes() > room) {
+            if (ln) ln = ln - 1 - ln / 16;  // shrink the prefixes until they fit
             if (ll) ll = ll - 1 - ll / 16;
+            if (lq) lq = lq - 1 - lq / 16;
         }
         mds->launch_lds_nodes = ln;
         mds->launch_lds_leaves = ll;
-        mds->launch_lds = lane_lds_bytes() + (size_t)ln * sizeof(TNode) + (size_t)ll * sizeof(TLeaf);
+        mds->launch_lds_quads = lq;
+        mds->launch_lds = lane_lds_bytes() + (size_t)bytes();
         int occ = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel_for(ds->feat), GS_BLOCK, mds->launch_lds));
         mds->per_cu = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
@@ -2017,6 +2277,7 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     const size_t lds = ds->launch_lds;
     a.lds_nodes = ds->launch_lds_nodes;
     a.lds_leaves = ds->launch_lds_leaves;
+    a.lds_quads = ds->launch_lds_quads;
     const int per_cu = g_blocks_per_cu > 0 ? g_blocks_per_cu : ds->per_cu;
     int64_t blocks = (int64_t)cus * per_cu;
     // no more waves than work: one lane per item at most

@@ -268,7 +268,7 @@ int64_t gs_host_struct_size(const char* name) {
     GS_SZ(gs_counters) GS_SZ(gs_node) GS_SZ(gs_sphere) GS_SZ(gs_msphere) GS_SZ(gs_quad) GS_SZ(gs_triangle)
     GS_SZ(gs_list) GS_SZ(gs_instance) GS_SZ(gs_medium) GS_SZ(gs_material) GS_SZ(gs_texture) GS_SZ(gs_image)
     GS_SZ(gs_background) GS_SZ(gs_flat_scene) GS_SZ(gs_camera) GS_SZ(gs_partition)
-    GS_SZ(gs_render_outputs) GS_SZ(gs_launch) GS_SZ(gs_multi_outputs) GS_SZ(gs_stats)
+    GS_SZ(gs_render_outputs) GS_SZ(gs_launch) GS_SZ(gs_multi_outputs) GS_SZ(gs_stats) GS_SZ(gs_scene_info)
 #undef GS_SZ
     return -1;
 }

@@ -191,6 +191,12 @@ class Renderer:
     def height(self):
         return self.cam.image_height
 
+    def scene_info(self):
+        """gs_device_scene_info as a dict (tree records, LDS mirror prefixes, kernel choices)."""
+        i = N.gs_scene_info()
+        N.check(N.lib.gs_device_scene_info(self.dev, C.byref(i)))
+        return {k: getattr(i, k) for k, _ in N.gs_scene_info._fields_}
+
     def render_async(self, d_packed, d_counters=0, stream=0, seed=1):
         """d_packed: device pointer to capacity*3 f32; d_counters: device gs_counters or 0."""
         N.check(N.lib.gs_render_tiles_async(self.dev, C.byref(self.cam), C.byref(self.settings), seed,

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 4
+#define GS_ABI_VERSION 5
 
 typedef int32_t gs_status;
 enum {
@@ -224,6 +224,11 @@ int32_t gs_version(void);
  * so only the association of the f64 colour sum differs from the sequential loop. */
 gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf_batch, int32_t sample_chunk);
 
+/* Node steps per traversal node pass, 1 .. 8 (ABI 4): a node pass lets every lane take
+ * up to this many BVH node steps before the wave re-checks which lanes sit at leaves.
+ * 0 (default) = the scene's own choice, from its tree's shape at gs_device_scene_create. */
+gs_status gs_set_node_steps(int32_t node_steps);
+
 /* Test hook: the auto sample-chunk rule's budget for chunk sums (default 4 GiB; 0
  * restores it).  A smaller budget makes renders take the chunk-doubling branch. */
 gs_status gs_debug_set_partial_budget(uint64_t bytes);
@@ -231,6 +236,24 @@ gs_status gs_debug_set_partial_budget(uint64_t bytes);
 /* Upload a flattened scene to the current HIP device. */
 gs_status gs_device_scene_create(const gs_flat_scene* scene, gs_device_scene** out);
 gs_status gs_device_scene_destroy(gs_device_scene* scene);
+
+/* What gs_device_scene_create built (ABI 5): the threaded top-level tree, the per-block
+ * LDS mirror prefixes (before any launch-time shrinking) and the kernel choices taken
+ * from the tree's shape.  nodes_per_leaf: expected node tests per leaf test of a ray
+ * that enters the root box (surface-area estimate: a record is tested with probability
+ * min over its ancestors' box areas / the root box's area); other_leaf_frac: the share of
+ * those leaf tests that are not stationary spheres (quads, triangles, lists, instances,
+ * media, moving spheres). */
+typedef struct gs_scene_info {
+    uint32_t node_records, leaf_records;
+    uint32_t lds_nodes, lds_leaves, lds_quads;
+    int32_t feat;       /* kernel features: 1 media, 2 nested BVHs, 4 sphere leaf runs */
+    int32_t node_steps; /* node steps per node pass the scene's launches use (see gs_set_node_steps) */
+    int32_t cert_boxes; /* every node coordinate |x| <= 1e15: the certified f32 box test applies */
+    double nodes_per_leaf;
+    double other_leaf_frac;
+} gs_scene_info;
+gs_status gs_device_scene_info(const gs_device_scene* scene, gs_scene_info* out);
 
 /* Number of packed pixels (tiles * tile_w * tile_h) this rank renders. */
 int64_t gs_partition_capacity(const gs_camera* cam, const gs_partition* part);

@@ -39,7 +39,7 @@ def test_every_declared_symbol_is_exported(built):
 
 
 def test_version_and_error_channel():
-    assert N.lib.gs_version() == N.GS_ABI_VERSION == 4
+    assert N.lib.gs_version() == N.GS_ABI_VERSION == 5
     assert N.lib.gs_set_tuning(0, 0, 0, -1) == N.GS_ERR_ARG
     assert b"tuning" in N.lib.gs_last_error()
     assert N.lib.gs_set_tuning(60, 0, 0, -1) == N.GS_OK
@@ -50,7 +50,8 @@ def test_version_and_error_channel():
 @pytest.mark.parametrize("name", ["gs_object", "gs_material_spec", "gs_texture_spec", "gs_image_spec",
                                   "gs_background_spec", "gs_scene_spec", "gs_camera_spec", "gs_sample_settings",
                                   "gs_counters", "gs_camera", "gs_partition", "gs_background", "gs_flat_scene",
-                                  "gs_render_outputs", "gs_launch", "gs_multi_outputs", "gs_stats"])
+                                  "gs_render_outputs", "gs_launch", "gs_multi_outputs", "gs_stats",
+                                  "gs_scene_info"])
 def test_struct_layouts_match(name):
     assert N.lib.gs_host_struct_size(name.encode()) == C.sizeof(getattr(N, name))
 
@@ -310,7 +311,7 @@ def test_rust_binding_declares_every_gpu_entry_point():
 
 
 @pytest.mark.parametrize("name", ["gs_counters", "gs_flat_scene", "gs_camera", "gs_render_outputs", "gs_medium",
-                                  "gs_launch", "gs_multi_outputs", "gs_stats"])
+                                  "gs_launch", "gs_multi_outputs", "gs_stats", "gs_scene_info"])
 def test_rust_struct_fields_follow_the_header(name):
     """Field names in declaration order (arrays flattened by name) match the C struct."""
     hdrs = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("grayshift_gpu.h", "grayshift_scene.h"))

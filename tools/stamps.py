@@ -14,16 +14,18 @@ def main():
     ap.add_argument("--shade-batch", type=int, default=52)
     ap.add_argument("--leaf-batch", type=int, default=12)
     ap.add_argument("--sample-chunk", type=int, default=-1)
+    ap.add_argument("--node-steps", type=int, default=0, help="0: the scene's own")
     a = ap.parse_args()
     import torch
     import grayshift_amd as g
     from grayshift_amd import _native as N, scenes
     g.set_tuning(a.shade_batch, 0, a.leaf_batch, a.sample_chunk)
+    N.check(N.lib.gs_set_node_steps(a.node_steps))
     sc = scenes.config(a.config, width=a.width, spp=a.spp)
     r = g.Renderer(sc, 0, 1, 64)
     dev = torch.device("cuda", 0)
     packed = torch.zeros(r.capacity * 3, dtype=torch.float32, device=dev)
-    dbg = torch.zeros(max(16, r.capacity // 2 + 2), dtype=torch.int64, device=dev)
+    dbg = torch.zeros(max(32, r.capacity // 2 + 2), dtype=torch.int64, device=dev)
     N.check(N.lib.gs_render_tiles_debug_async(r.dev, C.byref(r.cam), C.byref(r.settings), 1, C.byref(r.part),
                                               C.c_void_p(packed.data_ptr()), None, C.c_void_p(dbg.data_ptr()), None))
     torch.cuda.synchronize()
@@ -35,6 +37,11 @@ def main():
     print("traversal iterations %d: node passes %d (%.1f active lanes), leaf passes %d (%.1f lanes); "
           "shade passes %d (%.1f lanes)" % (it_all, it_node, ln_node / max(1, it_node), it_leaf,
                                            ln_leaf / max(1, it_leaf), it_shade, ln_shade / max(1, it_shade)))
+    node_clk, leaf_clk, dist_ref, dist_kind = dbg[15:19].cpu().tolist()
+    print("traversal split (wave clock, per-iteration stamps): node passes %.1f%%  leaf passes %.1f%%" % (
+        100.0 * node_clk / max(1, node_clk + leaf_clk), 100.0 * leaf_clk / max(1, node_clk + leaf_clk)))
+    print("leaf passes: %.2f distinct refs, %.2f distinct ref kinds per pass" % (
+        dist_ref / max(1, it_leaf), dist_kind / max(1, it_leaf)))
     reg = dbg[10:15].cpu().tolist()
     print("shade regions (%% of shade clock): " + "  ".join(
         "%s %.1f%%" % (n, 100.0 * x / max(1, v[2])) for n, x in
