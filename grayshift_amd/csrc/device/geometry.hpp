@@ -162,8 +162,8 @@ __device__ __forceinline__ bool box_hit_fast(const DNode& n, const d3& o, const 
 // the 1e-30 covers f32 underflow.  All values stay finite (|t'| < 2e30), so no NaN.
 #define GS_CERT_K 4.76837158203125e-07f  // 2^-21
 
-struct alignas(16) TNode {  // 32 B record of the threaded tree: f32 box + hit / miss links
-    float mnx, mny, mnz, mxx, mxy, mxz;
+struct alignas(16) TNode {  // 32 B record of the threaded tree: f32 box (paired for box_cert) + hit / miss links
+    float mnx, mny, mxx, mxy, mnz, mxz;
     uint32_t hit, miss;
 };
 struct alignas(16) TLeaf {  // 48 B leaf record: a stationary sphere inline, next link, ABI ref
@@ -181,10 +181,14 @@ struct alignas(16) TQuad {
     double qx, qy, qz, ux, uy, uz, vx, vy, vz, wx, wy, wz;
 };
 
+typedef float gs_f2 __attribute__((ext_vector_type(2)));
+// Per-ray constants of the certified test, paired so that one packed FMA (v_pk_fma_f32:
+// the issue cost of one v_fma_f32, measured on MI355X) computes two planes: (min x, min
+// y), (max x, max y) with the (x, y) pairs, (min z, max z) with the z pairs.
 struct RayCert {
-    float ix, iy, iz;  // f32(1/d)
-    float ox, oy, oz;  // f32(-(o * (1/d)))
-    float r2;          // 2 K R + 1e-30
+    gs_f2 ixy, oxy;  // f32(1/d), f32(-(o * (1/d))) of x and y
+    gs_f2 izz, ozz;  // those of z, twice
+    float r2;        // 2 K R + 1e-30
 };
 
 __host__ __device__ __forceinline__ bool cert_ray_ok(const d3& o, const d3& inv) {
@@ -195,22 +199,22 @@ __host__ __device__ __forceinline__ bool cert_ray_ok(const d3& o, const d3& inv)
 __device__ __forceinline__ RayCert make_cert(const d3& o, const d3& inv) {
     RayCert c;
     const double px = o.x * inv.x, py = o.y * inv.y, pz = o.z * inv.z;
-    c.ix = (float)inv.x;
-    c.iy = (float)inv.y;
-    c.iz = (float)inv.z;
-    c.ox = (float)(-px);
-    c.oy = (float)(-py);
-    c.oz = (float)(-pz);
     const double R = __builtin_fmax(__builtin_fabs(px), __builtin_fmax(__builtin_fabs(py), __builtin_fabs(pz)));
+    c.ixy = gs_f2{(float)inv.x, (float)inv.y};
+    c.oxy = gs_f2{(float)(-px), (float)(-py)};
+    c.izz = gs_f2{(float)inv.z, (float)inv.z};
+    c.ozz = gs_f2{(float)(-pz), (float)(-pz)};
     c.r2 = (float)(2.0 * (double)GS_CERT_K * R * (1.0 + 0x1p-20)) + 1e-30f;
     return c;
 }
 // Returns the certified decision (hit); `undecided` when f32 cannot decide (run the f64 test).
 __device__ __forceinline__ bool box_cert(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
                                          const RayCert& c, float tmin32, float closest32, bool& undecided) {
-    const float t0x = __builtin_fmaf(mnx, c.ix, c.ox), t1x = __builtin_fmaf(mxx, c.ix, c.ox);
-    const float t0y = __builtin_fmaf(mny, c.iy, c.oy), t1y = __builtin_fmaf(mxy, c.iy, c.oy);
-    const float t0z = __builtin_fmaf(mnz, c.iz, c.oz), t1z = __builtin_fmaf(mxz, c.iz, c.oz);
+    // t = fma(coordinate, 1/d, -o/d) for both planes of an axis at once
+    const gs_f2 t0 = __builtin_elementwise_fma(gs_f2{mnx, mny}, c.ixy, c.oxy);
+    const gs_f2 t1 = __builtin_elementwise_fma(gs_f2{mxx, mxy}, c.ixy, c.oxy);
+    const gs_f2 tz = __builtin_elementwise_fma(gs_f2{mnz, mxz}, c.izz, c.ozz);
+    const float t0x = t0.x, t1x = t1.x, t0y = t0.y, t1y = t1.y, t0z = tz.x, t1z = tz.y;
     const float lo = __builtin_fmaxf(__builtin_fmaxf(tmin32, __builtin_fminf(t0x, t1x)),
                                      __builtin_fmaxf(__builtin_fminf(t0y, t1y), __builtin_fminf(t0z, t1z)));
     const float hi = __builtin_fminf(__builtin_fminf(closest32, __builtin_fmaxf(t0x, t1x)),
