@@ -142,9 +142,11 @@ __device__ __forceinline__ bool box_hit_fast(const DNode& n, const d3& o, const 
 // must reproduce every decision (node visits and primitive tests equal the oracle's).
 // But nearly every decision is far from its tie: the f32 form below decides it with a
 // proven error bound and reports "undecided" otherwise, and only undecided lanes run the
-// f64 test.  Half-rate f64 on gfx950 makes the f32 form (one FMA per slab plane) ~2.5x
-// cheaper in VALU cycles than the f64 one, and its 32-B node record doubles what the LDS
-// mirror holds.
+// f64 test.  The f32 form takes fewer instructions — one FMA per slab plane (two per
+// packed FMA) against a subtract and a multiply, 32-bit min/max against 64-bit ones — while
+// MI355X issues f64 and f32 add/mul/FMA at about the same cost per wave-instruction
+// (tools/ubench/valu_rate.hip: 4.9 / 5.7 cycles per SIMD at 4 waves); and its 32-B node
+// record doubles what the LDS mirror holds (C4: 4673 -> 5263 Msamples/s).
 //
 // Per ray (rays with every |1/d| in [1e-25, 1e15] and |o| <= 1e15, scenes with every
 // node coordinate |x| <= 1e15: "cert rays"): ix = f32(1/d), ox = f32(-(o * (1/d))) (the
