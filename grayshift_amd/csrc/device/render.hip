@@ -883,6 +883,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     float closest32 = 0.0f;  // f32(closest)
     const float tmin32 = 0.001f;  // f32(tmin)
     bool fast = false;  // a cert ray: nodes take box_cert (geometry.hpp)
+    // The lane has a new ray in `ray` whose traversal state begin_ray has not set up yet:
+    // camera rays (advance) and scattered rays (shade) meet in one begin_ray per phase, so
+    // a wave pays for it once, not once per branch.
+    bool fresh = false;
     // hot counters kept in registers, flushed per pixel
     uint32_t c_nodes = 0, c_sph = 0;  // (per lane: one VALU add beat a 64-bit SALU wave count)
 
@@ -1002,7 +1006,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             Tr = Tg = Tb = 1.0;
             LI(L_DEPTH) = cam.max_depth;
             if (cam.max_depth > 0) {
-                begin_ray();
+                fresh = true;  // begin_ray by the caller
                 st = S_TRACE;
                 return;
             }
@@ -1110,6 +1114,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 }
             }
             need = __builtin_amdgcn_ballot_w64(st == S_NEED);
+        }
+        if (fresh) {
+            begin_ray();
+            fresh = false;
         }
         if (st == S_NEED) st = S_DONE;
         if (__builtin_amdgcn_ballot_w64(st == S_TRACE || st == S_SHADE) == 0) break;
@@ -1351,9 +1359,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     if (depth > 0) {
                         ray.o = h.p;
                         ray.d = s.dir;
-                        GS_STAMP(r0);
-                        begin_ray();
-                        GS_REGION(3, r0);
+                        fresh = true;
                         st = S_TRACE;
                         ends = false;
                     }  // else ray_color(.., 0) = 0 (camera.rs:175): black
@@ -1370,6 +1376,15 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 advance();
                 GS_REGION(4, r0);
             }
+        }
+        if (fresh) {  // scattered and new camera rays together
+#ifdef GS_STAMPS
+            uint64_t r0;
+#endif
+            GS_STAMP(r0);
+            begin_ray();
+            GS_REGION(3, r0);
+            fresh = false;
         }
 #ifdef GS_STAMPS
         GS_STAMP(ts3);
