@@ -45,8 +45,16 @@ __device__ __forceinline__ uint64_t wy_next(uint64_t& state) {
     uint64_t s = state + C0;
     state = s;
     uint64_t b = s ^ C1;
-    uint64_t lo = s * b;
-    uint64_t hi = __umul64hi(s, b);
+    // The 128-bit product s * b from four 32x32->64 partial products, each a
+    // v_mad_u64_u32 with its carry-in folded into the addend: the low half reuses the
+    // partial products the high half needs (`s * b` and __umul64hi compiled separately
+    // recomputed two of them: 22 -> 19 VALU per draw on gfx950).
+    const uint32_t s0 = (uint32_t)s, s1 = (uint32_t)(s >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const uint64_t p00 = (uint64_t)s0 * b0;
+    const uint64_t t = (uint64_t)s0 * b1 + (p00 >> 32);
+    const uint64_t u = (uint64_t)s1 * b0 + (uint32_t)t;
+    const uint64_t hi = (uint64_t)s1 * b1 + ((t >> 32) + (u >> 32));
+    const uint64_t lo = (u << 32) | (uint32_t)p00;
     return lo ^ hi;
 }
 __device__ __forceinline__ double wy_f64(uint64_t& state) {
@@ -62,6 +70,28 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 // Per-(pixel, sample) stream.
 __device__ __forceinline__ uint64_t stream_seed(uint64_t seed, uint32_t pixel, uint32_t sample) {
     return splitmix64(seed ^ splitmix64(((uint64_t)sample << 32) | (uint64_t)pixel));
+}
+
+// Unsigned 32-bit division by a divisor fixed for a launch (image width, tiles per row,
+// chunks per pixel, ...): the round-up multiply-shift method (Granlund & Montgomery
+// 1994; Hacker's Delight 10-8), exact for every n < 2^32 and every d >= 1 -- 5 VALU
+// instead of the ~18 of a division by a runtime value.  The host fills the magic.
+struct UDiv {
+    uint32_t d, m, s1, s2;
+};
+__host__ __device__ inline UDiv udiv_make(uint32_t d) {
+    uint32_t l = 0;
+    while (l < 32 && (1ull << l) < d) l++;  // ceil(log2 d)
+    UDiv u;
+    u.d = d;
+    u.m = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+    u.s1 = l < 1 ? l : 1;
+    u.s2 = l < 1 ? 0 : l - 1;
+    return u;
+}
+__device__ __forceinline__ uint32_t udiv(uint32_t n, const UDiv& u) {
+    const uint32_t t = __umulhi(n, u.m);
+    return (t + ((n - t) >> u.s1)) >> u.s2;
 }
 
 // Rust `f64 as i32` (saturating, NaN -> 0).

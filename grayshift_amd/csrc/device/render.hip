@@ -63,6 +63,10 @@ using namespace gsd;
 #define GS_FEAT_LEAFRUN 4 // sphere leaves come in adjacent pairs: leaf passes test runs of them
 #define GS_FEAT_LDSTREE 8 // every record of the threaded tree is in the LDS mirror: no global path
                           // (instantiated without media / nested BVHs only; C3 +1%, C5 +2.5%)
+#define GS_FEAT_MIXED 16  // three or more of {sky, Lambertian, metal, dielectric, isotropic}:
+                          // staged shading (shade), else one branch per case (shade_split);
+                          // media / nested-BVH scenes always stage.  MI355X: C4 +2.2%, C5 +1.6%
+                          // staged, C3 (Lambertian + light) -2.8% staged
 
 // ---------------------------------------------------------------- device layout
 // Internal layouts (may differ from the ABI records; converted at upload).
@@ -80,6 +84,14 @@ enum {
     DM_ISO_SOLID = 8,     // Isotropic over a solid: a = albedo  (material.rs:185-196)
     DM_ISO_TEX = 9        // Isotropic over `texture`
 };
+// ISA census build only (-DGS_ISA_MARKS, tools/isa_census.py): assembler comments that
+// delimit the node pass, its f64 fallback and the leaf pass in the generated code.
+#ifdef GS_ISA_MARKS
+#define GS_MARK(s) asm volatile(";; GS_MARK " s)
+#else
+#define GS_MARK(s) do { } while (0)
+#endif
+
 struct alignas(16) DMaterial {
     uint32_t kind, texture, needs_uv, pad;
     double a[3];
@@ -129,6 +141,9 @@ struct KParams {
     // pixel running the reference's batch loop (camera.rs:135-165) to completion.
     uint32_t chunk, cpp, n_items;
     uint32_t claim;  // work items a wave claims per queue atomic (its private reserve)
+    // multiply-shift forms of the launch's fixed divisors (devmath.hpp UDiv): chunks per
+    // pixel, tile pixels, 8x8 blocks per tile row, tile width, tiles per row, image width
+    UDiv u_cpp, u_tpx, u_bpr, u_tw, u_tx, u_w;
     const int32_t* order;  // position -> tile (gs_partition.d_tile_order), or null: tile = position
     double* partial;
     float* out;     // linear colour per packed pixel (nullable when out8 is set)
@@ -651,19 +666,18 @@ __device__ GS_NOINLINE d3 texture_value(const DevScene& sc, uint32_t tex, double
     return mk(0.0, 0.0, 0.0);
 }
 
-// Camera::sample_background / HDRI::sample (camera.rs:228-233, 257-270).
-__device__ GS_NOINLINE d3 background(const DevScene& sc, d3 dir, unsigned long long* cnt) {
+// HDRI::sample's texel (camera.rs:257-270) for an already normalised, rotated direction.
+__device__ __forceinline__ d3 hdri_texel(const DevScene& sc, d3 rot, unsigned long long* cnt) {
     const gs_background& bg = sc.bg;
-    if (bg.kind == GS_BG_SOLID) return ld3(bg.color);
     const double PI = 3.14159265358979323846;
-    d3 rv = mk(dir.x * bg.rot[0] + dir.y * bg.rot[1] + dir.z * bg.rot[2],
-               dir.x * bg.rot[3] + dir.y * bg.rot[4] + dir.z * bg.rot[5],
-               dir.x * bg.rot[6] + dir.y * bg.rot[7] + dir.z * bg.rot[8]);
     uint64_t x, y;
     {
-        d3 rot = unit(rv);
+#ifdef GS_ABL_SKY  // ablation build (A/B only, wrong sky): no atan2 / asin
+        double theta = rot.y * 3.0, phi = rot.z;
+#else
         double theta = atan2(rot.y, rot.x);
         double phi = asin(rot.z);
+#endif
         double u = 0.5 + theta / (2.0 * PI);
         double v = 0.5 - phi / PI;
         x = sat_u64(u * (double)bg.width, 18446744073709551616.0, ~0ull) % (uint64_t)bg.width;
@@ -681,6 +695,192 @@ __device__ GS_NOINLINE d3 background(const DevScene& sc, d3 dir, unsigned long l
     }
     const float* px = sc.hdri + k * 3;
     return mk((double)px[0], (double)px[1], (double)px[2]);
+}
+
+__device__ __forceinline__ d3 checker(const DMaterial& m, d3 p) {  // texture.rs:58-70
+    int32_t xi = sat_i32(floor(m.param * p.x));
+    int32_t yi = sat_i32(floor(m.param * p.y));
+    int32_t zi = sat_i32(floor(m.param * p.z));
+    int32_t s = (int32_t)((uint32_t)xi + (uint32_t)yi + (uint32_t)zi);
+    return (s % 2 == 0) ? ld3(m.a) : ld3(m.b);
+}
+
+// One shading lane: a miss (Camera::sample_background, camera.rs:201,228-233) or a hit
+// (the HitRecord, then Material::emitted / scatter, material.rs).  cont = 1: the path
+// continues from p along dir with attenuation col; cont = 0: it ends with radiance col
+// (sky or emitted colour; 0 for an absorbed ray).
+struct ShadeOut {
+    d3 col, dir;
+    uint32_t cont;
+};
+
+// Written as stages every shading lane passes through together, whatever its case, so
+// a wave holding several cases pays once for the work they share instead of once per
+// divergent branch: one unit() for the first normalisation (the rotated sky direction,
+// the Lambertian ONB's w, the metal reflection, the dielectric's unit direction), one
+// sqrt and division for the second (the ONB's v axis, random_unit_vector, and the
+// dielectric's sin θ), one sqrt for the third (the cosine direction's unit, refract's
+// parallel part), and one RNG draw for the Lambertian's r1 and the dielectric's Schlick
+// draw.  Every lane evaluates exactly the reference's expressions on the same operands
+// in the same order; only which lanes issue an instruction together changes.
+// A hit lane's ray.o becomes the hit point p (the next ray's origin) as soon as p is
+// known: nothing after the HitRecord reads the old origin, and p need not stay live.
+__device__ __forceinline__ ShadeOut shade(const DevScene& sc, Ray& ray, double t, uint32_t hit_ref,
+                                          uint32_t hit_inst, uint64_t& rng, unsigned long long* cnt) {
+    const double PI = 3.14159265358979323846;
+    ShadeOut o;
+    o.cont = 0;
+    o.col = mk(0.0, 0.0, 0.0);
+    o.dir = mk(0.0, 0.0, 0.0);
+    const bool miss = hit_ref == GS_REF_NONE;
+    HitRec h;
+    h.p = h.n = mk(0.0, 0.0, 0.0);
+    h.u = h.v = 0.0;
+    h.front = false;
+    uint32_t kind = 0;  // 0: a miss
+    const DMaterial* m = sc.mats;
+    if (!miss) {
+        atomicAdd(&cnt[C_HITS], 1ull);
+        h = reconstruct(sc, ray, t, hit_ref, hit_inst);
+        m = &sc.mats[h.mat];
+        kind = m->kind;
+        ray.o = h.p;
+    }
+    const bool lamb = kind >= DM_LAMB_SOLID && kind <= DM_LAMB_TEX;  // material.rs:45-68
+    const bool metal = kind == DM_METAL;                              // :87-102
+    const bool diel = kind == DM_DIELECTRIC;                          // :123-148
+    const bool iso = kind == DM_ISO_SOLID || kind == DM_ISO_TEX;      // :185-196
+    const bool sky = miss && sc.bg.kind != GS_BG_SOLID;
+
+    // albedo / emitted colour (texture.rs:27-95): one texture_value call site for every kind
+    if (kind == DM_LAMB_TEX || kind == DM_LIGHT_TEX || kind == DM_ISO_TEX) {
+        o.col = texture_value(sc, m->texture, h.u, h.v, h.p, cnt);
+    } else if (kind == DM_LAMB_CHECKER) {
+        o.col = checker(*m, h.p);
+    } else if (kind == DM_DIELECTRIC) {
+        o.col = mk(1.0, 1.0, 1.0);
+    } else if (!miss) {
+        o.col = ld3(m->a);
+    } else if (!sky) {
+        o.col = ld3(sc.bg.color);
+    }
+
+    // stage 1: the first normalisation
+    d3 v1 = mk(1.0, 0.0, 0.0);
+    if (sky) {
+        const double* R = sc.bg.rot;
+        const d3 dir = ray.d;
+        v1 = mk(dir.x * R[0] + dir.y * R[1] + dir.z * R[2], dir.x * R[3] + dir.y * R[4] + dir.z * R[5],
+                dir.x * R[6] + dir.y * R[7] + dir.z * R[8]);
+    } else if (lamb) {
+        v1 = h.n;  // OrthonormalBasis::new (ONB.rs:10-23): w = unit(n)
+    } else if (metal) {
+        v1 = reflect(ray.d, h.n);
+    } else if (diel) {
+        v1 = ray.d;
+    }
+    const d3 u1 = unit(v1);
+
+    // stage 2: the sky texel; the second vector to normalise (or sin θ's argument)
+    d3 v2 = mk(1.0, 0.0, 0.0);
+    double q2 = 1.0, ri = 0.0, cos_theta = 0.0;
+    if (sky) {
+        o.col = hdri_texel(sc, u1, cnt);
+    } else if (lamb) {
+        const d3 a = fabs(u1.x) > 0.9 ? mk(0.0, 1.0, 0.0) : mk(1.0, 0.0, 0.0);
+        v2 = cross(u1, a);
+        q2 = len2(v2);
+    } else if (metal || iso) {  // random_unit_vector (util.rs:18-29)
+#pragma unroll 1
+        for (;;) {
+            double x = wy_f64(rng) * 2.0 + -1.0;
+            double y = wy_f64(rng) * 2.0 + -1.0;
+            double z = wy_f64(rng) * 2.0 + -1.0;
+            v2 = mk(x, y, z);
+            q2 = len2(v2);
+            if (q2 < 1.0) break;
+        }
+    } else if (diel) {
+        ri = h.front ? 1.0 / m->param : m->param;
+        cos_theta = fmin(dot(neg(u1), h.n), 1.0);
+        q2 = 1.0 - cos_theta * cos_theta;
+    }
+    const double r2v = sqrt(q2);  // |v2|, or the dielectric's sin θ
+    d3 u2 = v2;
+    if (lamb || metal || iso) u2 = divs(v2, r2v);
+
+    // stage 3: the scattered direction
+    double rd = 0.0;  // the first draw: the Lambertian's r1, the dielectric's Schlick draw
+    if (lamb || diel) rd = wy_f64(rng);
+    d3 w3 = mk(0.0, 0.0, 0.0), n3 = h.n;
+    double q3 = 1.0;
+    bool third = false;  // the lane finishes with the stage-3 sqrt
+    if (lamb) {
+        // random_cosine_direction (util.rs:48-60), r2^(1/4) quirk kept; ONB transform
+        const d3 vv = u2;
+        const d3 uu = cross(u1, vv);
+        double r1 = rd;
+        double r2 = wy_f64(rng);
+        double phi = 2.0 * PI * r1;
+        double r2s = sqrt(r2);
+        double sp, cp;
+        sincos(phi, &sp, &cp);
+        double q = sqrt(r2s);
+        d3 cd = mk(cp * q, sp * q, sqrt(1.0 - r2));
+        w3 = add(add(muls(uu, cd.x), muls(vv, cd.y)), muls(u1, cd.z));
+        q3 = len2(w3);
+        third = true;
+        o.cont = 1;
+    } else if (metal) {
+        const d3 reflected = add(u1, muls(u2, m->param));
+        if (dot(reflected, h.n) > 0.0) {
+            o.dir = reflected;
+            o.cont = 1;
+        } else {
+            o.col = mk(0.0, 0.0, 0.0);  // absorbed
+        }
+    } else if (iso) {
+        o.dir = u2;
+        o.cont = 1;
+    } else if (diel) {
+        const d3 ud = u1;
+        double sin_theta = r2v;
+        bool cannot_refract = ri * sin_theta > 1.0;
+        double r0 = (1.0 - ri) / (1.0 + ri);
+        r0 = r0 * r0;
+        double x = 1.0 - cos_theta;
+        double x2 = x * x;
+        double x4 = x2 * x2;
+        double refl = r0 + (1.0 - r0) * (x * x4);  // powi(x, 5) as LLVM expands it
+        bool fresnel = refl > rd;
+        if (cannot_refract || fresnel) {
+            o.dir = reflect(ud, h.n);
+        } else {  // refract (vec3.rs:57-62)
+            double ct = fmin(dot(h.n, neg(ud)), 1.0);
+            w3 = muls(add(ud, muls(h.n, ct)), ri);
+            q3 = fabs(1.0 - len2(w3));
+            third = true;
+        }
+        o.cont = 1;
+    }
+    if (third) {
+        const double r3 = sqrt(q3);
+        if (lamb) o.dir = divs(w3, r3);                    // unit(cosine direction)
+        else o.dir = add(w3, muls(n3, -r3));               // r_out_perp + r_out_parallel
+    }
+    return o;
+}
+
+// ---- split shading (scenes with at most two of: sky, Lambertian, metal, dielectric,
+// isotropic): one divergent branch per case, no select overhead.
+// Camera::sample_background / HDRI::sample (camera.rs:228-233, 257-270).
+__device__ GS_NOINLINE d3 background(const DevScene& sc, d3 dir, unsigned long long* cnt) {
+    const gs_background& bg = sc.bg;
+    if (bg.kind == GS_BG_SOLID) return ld3(bg.color);
+    d3 rv = mk(dir.x * bg.rot[0] + dir.y * bg.rot[1] + dir.z * bg.rot[2],
+               dir.x * bg.rot[3] + dir.y * bg.rot[4] + dir.z * bg.rot[5],
+               dir.x * bg.rot[6] + dir.y * bg.rot[7] + dir.z * bg.rot[8]);
+    return hdri_texel(sc, unit(rv), cnt);
 }
 
 __device__ __forceinline__ d3 random_unit_vector(uint64_t& rng) {  // util.rs:18-29
@@ -704,14 +904,6 @@ struct Scatter {
     uint64_t rng;
     uint32_t cont;
 };
-
-__device__ __forceinline__ d3 checker(const DMaterial& m, d3 p) {  // texture.rs:58-70
-    int32_t xi = sat_i32(floor(m.param * p.x));
-    int32_t yi = sat_i32(floor(m.param * p.y));
-    int32_t zi = sat_i32(floor(m.param * p.z));
-    int32_t s = (int32_t)((uint32_t)xi + (uint32_t)yi + (uint32_t)zi);
-    return (s % 2 == 0) ? ld3(m.a) : ld3(m.b);
-}
 
 __device__ GS_NOINLINE Scatter scatter(const DevScene& sc, HitRec h, d3 in_dir, uint64_t rng,
                                         unsigned long long* cnt) {
@@ -795,13 +987,6 @@ __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull <<
 #define GS_REGION(k, t0) do { } while (0)
 #endif
 
-// ISA census build only (-DGS_ISA_MARKS, tools/isa_census.py): assembler comments that
-// delimit the node pass, its f64 fallback and the leaf pass in the generated code.
-#ifdef GS_ISA_MARKS
-#define GS_MARK(s) asm volatile(";; GS_MARK " s)
-#else
-#define GS_MARK(s) do { } while (0)
-#endif
 
 // Per-lane pixel state lives in LDS ([field][lane], conflict-free), touched once per
 // path; the mirror of the tree's top records follows it.
@@ -979,7 +1164,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             }
             // Camera::get_ray (camera.rs:204-221) on the seeded stream of this sample
             const uint32_t pix = LI(L_PIX);
-            const uint32_t pi = pix % (uint32_t)cam.image_width, pj = pix / (uint32_t)cam.image_width;
+            const uint32_t pj = udiv(pix, P->u_w), pi = pix - pj * (uint32_t)cam.image_width;
             rng = stream_seed(P->seed, pix, LI(L_SAMPLE));
             atomicAdd(&s_cnt[C_PATHS], 1ull);
             double offx = wy_f64(rng) - 0.5;
@@ -1057,24 +1242,25 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     // work order: 8x8 blocks inside each tile (coherent primary rays), a
                     // pixel's chunks adjacent
                     const uint32_t cpp = P->cpp;
-                    const uint32_t pq = (uint32_t)(q / cpp), ck = (uint32_t)(q % cpp);
-                    const uint32_t slot = pq / tile_px, w = pq % tile_px;
+                    const uint32_t q32 = (uint32_t)q;  // q < n_items < 2^32
+                    const uint32_t pq = udiv(q32, P->u_cpp), ck = q32 - pq * cpp;
+                    const uint32_t slot = udiv(pq, P->u_tpx), w = pq - slot * tile_px;
                     uint32_t x, y;
                     if (blocked8) {
                         const uint32_t b = w >> 6, l = w & 63, bpr = (uint32_t)P->tile_w >> 3;
-                        x = (b % bpr) * 8 + (l & 7);
-                        y = (b / bpr) * 8 + (l >> 3);
+                        const uint32_t by = udiv(b, P->u_bpr);
+                        x = (b - by * bpr) * 8 + (l & 7);
+                        y = by * 8 + (l >> 3);
                     } else {
-                        x = w % (uint32_t)P->tile_w;
-                        y = w / (uint32_t)P->tile_w;
+                        y = udiv(w, P->u_tw);
+                        x = w - y * (uint32_t)P->tile_w;
                     }
                     const uint32_t item = slot * tile_px + y * (uint32_t)P->tile_w + x;
                     const uint32_t pos = (uint32_t)P->rank + slot * (uint32_t)P->world_size;
                     const uint32_t tile = P->order ? (uint32_t)P->order[pos] : pos;  // -1: empty slot
-                    const uint32_t pi = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu
-                                                            : (tile % (uint32_t)P->tiles_x) * (uint32_t)P->tile_w + x;
-                    const uint32_t pj = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu
-                                                            : (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + y;
+                    const uint32_t ty = udiv(tile, P->u_tx), tx = tile - ty * (uint32_t)P->tiles_x;
+                    const uint32_t pi = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu : tx * (uint32_t)P->tile_w + x;
+                    const uint32_t pj = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu : ty * (uint32_t)P->tile_h + y;
                     if (pi >= (uint32_t)cam.image_width || pj >= (uint32_t)cam.image_height) {
                         if (!P->chunk) {  // padding pixel (chunked: gs_combine_kernel writes it)
                             if (P->out) {
@@ -1333,23 +1519,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #ifdef GS_STAMPS
             uint64_t r0;
 #endif
-            if (hit_ref == GS_REF_NONE) {
-                // miss: sample_background (camera.rs:201); the path's only radiance
+            if constexpr ((FEAT & (GS_FEAT_MIXED | GS_FEAT_MEDIA | GS_FEAT_NESTED)) != 0) {
                 GS_STAMP(r0);
-                const d3 bg = background(sc, ray.d, s_cnt);
-                GS_REGION(0, r0);
-                Lr = Tr * bg.x;
-                Lg = Tg * bg.y;
-                Lb = Tb * bg.z;
-            } else {
-                atomicAdd(&s_cnt[C_HITS], 1ull);
-                GS_STAMP(r0);
-                const HitRec h = reconstruct(sc, ray, closest, hit_ref, LI(L_HINST));
-                GS_REGION(1, r0);
-                GS_STAMP(r0);
-                const Scatter s = scatter(sc, h, ray.d, rng, s_cnt);
+                GS_MARK("shade_begin");
+                const ShadeOut s = shade(sc, ray, closest, hit_ref, LI(L_HINST), rng, s_cnt);
+                GS_MARK("shade_end");
                 GS_REGION(2, r0);
-                rng = s.rng;
                 if (s.cont) {
                     Tr = Tr * s.col.x;
                     Tg = Tg * s.col.y;
@@ -1357,23 +1532,62 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     const uint32_t depth = LI(L_DEPTH) - 1u;
                     LI(L_DEPTH) = depth;
                     if (depth > 0) {
-                        ray.o = h.p;
-                        ray.d = s.dir;
+                        ray.d = s.dir;  // (ray.o = p: set by shade)
                         fresh = true;
                         st = S_TRACE;
                         ends = false;
                     }  // else ray_color(.., 0) = 0 (camera.rs:175): black
                 } else {
-                    // emitter (DiffuseLight never scatters) or absorbed (col = 0)
+                    // sky (camera.rs:201), emitter (DiffuseLight never scatters) or absorbed (col = 0)
                     Lr = Tr * s.col.x;
                     Lg = Tg * s.col.y;
                     Lb = Tb * s.col.z;
                 }
+            } else {  // split: one branch per case
+                if (hit_ref == GS_REF_NONE) {
+                    // miss: sample_background (camera.rs:201); the path's only radiance
+                    GS_STAMP(r0);
+                    const d3 bg = background(sc, ray.d, s_cnt);
+                    GS_REGION(0, r0);
+                    Lr = Tr * bg.x;
+                    Lg = Tg * bg.y;
+                    Lb = Tb * bg.z;
+                } else {
+                    atomicAdd(&s_cnt[C_HITS], 1ull);
+                    GS_STAMP(r0);
+                    const HitRec h = reconstruct(sc, ray, closest, hit_ref, LI(L_HINST));
+                    GS_REGION(1, r0);
+                    GS_STAMP(r0);
+                    const Scatter s = scatter(sc, h, ray.d, rng, s_cnt);
+                    GS_REGION(2, r0);
+                    rng = s.rng;
+                    if (s.cont) {
+                        Tr = Tr * s.col.x;
+                        Tg = Tg * s.col.y;
+                        Tb = Tb * s.col.z;
+                        const uint32_t depth = LI(L_DEPTH) - 1u;
+                        LI(L_DEPTH) = depth;
+                        if (depth > 0) {
+                            ray.o = h.p;
+                            ray.d = s.dir;
+                            fresh = true;
+                            st = S_TRACE;
+                            ends = false;
+                        }  // else ray_color(.., 0) = 0 (camera.rs:175): black
+                    } else {
+                        // emitter (DiffuseLight never scatters) or absorbed (col = 0)
+                        Lr = Tr * s.col.x;
+                        Lg = Tg * s.col.y;
+                        Lb = Tb * s.col.z;
+                    }
+                }
             }
             if (ends) {
                 GS_STAMP(r0);
+                GS_MARK("adv_begin");
                 add_sample(Lr, Lg, Lb);
                 advance();
+                GS_MARK("adv_end");
                 GS_REGION(4, r0);
             }
         }
@@ -1382,7 +1596,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             uint64_t r0;
 #endif
             GS_STAMP(r0);
+            GS_MARK("br_begin");
             begin_ray();
+            GS_MARK("br_end");
             GS_REGION(3, r0);
             fresh = false;
         }
@@ -2129,6 +2345,17 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ds->feat = (s->n_media != 0 ? GS_FEAT_MEDIA : 0) | (nested ? GS_FEAT_NESTED : 0) | (leaf_runs ? GS_FEAT_LEAFRUN : 0);
     if (!(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED)) && lds_nodes == tnodes.size() && lds_leaves == tleaves.size())
         ds->feat |= GS_FEAT_LDSTREE;  // (cleared at launch if the device's LDS cannot hold it all)
+    {  // staged shading when three or more of its sharing cases can meet in one wave
+        bool lamb = false, metal = false, diel = false, iso = false;
+        for (const DMaterial& m : mats) {
+            lamb |= m.kind >= DM_LAMB_SOLID && m.kind <= DM_LAMB_TEX;
+            metal |= m.kind == DM_METAL;
+            diel |= m.kind == DM_DIELECTRIC;
+            iso |= m.kind == DM_ISO_SOLID || m.kind == DM_ISO_TEX;
+        }
+        const int cases = (int)lamb + (int)metal + (int)diel + (int)iso + (int)(s->background.kind != GS_BG_SOLID);
+        if (cases >= 3 && !(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED))) ds->feat |= GS_FEAT_MIXED;
+    }
     ds->cert_boxes = cert_boxes;
     ds->node_steps = auto_node_steps;
     *out = ds;
@@ -2194,6 +2421,11 @@ static void (*kernel_for(int feat))(KArgs) {
             return gs_render_kernel<GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED>;
         case GS_FEAT_LDSTREE: return gs_render_kernel<GS_FEAT_LDSTREE>;
         case GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN: return gs_render_kernel<GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN>;
+        case GS_FEAT_MIXED: return gs_render_kernel<GS_FEAT_MIXED>;
+        case GS_FEAT_MIXED | GS_FEAT_LEAFRUN: return gs_render_kernel<GS_FEAT_MIXED | GS_FEAT_LEAFRUN>;
+        case GS_FEAT_MIXED | GS_FEAT_LDSTREE: return gs_render_kernel<GS_FEAT_MIXED | GS_FEAT_LDSTREE>;
+        case GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN:
+            return gs_render_kernel<GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN>;
         default: return gs_render_kernel<0>;
     }
 }
@@ -2259,6 +2491,12 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     kp.chunk = chunk;
     kp.cpp = cpp;
     kp.n_items = (uint32_t)cap * cpp;
+    kp.u_cpp = udiv_make(cpp);
+    kp.u_tpx = udiv_make((uint32_t)(part->tile_w * part->tile_h));
+    kp.u_bpr = udiv_make(std::max<uint32_t>(1, (uint32_t)part->tile_w >> 3));
+    kp.u_tw = udiv_make((uint32_t)part->tile_w);
+    kp.u_tx = udiv_make((uint32_t)kp.tiles_x);
+    kp.u_w = udiv_make((uint32_t)cam->image_width);
     kp.claim = 1;  // set below, once the grid size is known
     kp.out = outs->rgb;
     kp.out8 = outs->rgb8;

@@ -43,9 +43,11 @@ def main():
     print("leaf passes: %.2f distinct refs, %.2f distinct ref kinds per pass" % (
         dist_ref / max(1, it_leaf), dist_kind / max(1, it_leaf)))
     reg = dbg[10:15].cpu().tolist()
+    # split shading (no GS_FEAT_MIXED) stamps background / reconstruct / scatter on their own;
+    # staged shading (GS_FEAT_MIXED, media, nested) stamps all of it as region 2
     print("shade regions (%% of shade clock): " + "  ".join(
         "%s %.1f%%" % (n, 100.0 * x / max(1, v[2])) for n, x in
-        zip(["background", "reconstruct", "scatter", "begin_ray", "sample+advance"], reg)))
+        zip(["background", "reconstruct", "scatter (staged: all shading)", "begin_ray", "sample+advance"], reg)))
 
 
 if __name__ == "__main__":
