@@ -258,6 +258,44 @@ __device__ __forceinline__ bool sphere_accept(d3 c, double r, const Ray& ray, do
     return true;
 }
 
+// HDRI::sample's texel column and row (camera.rs:257-270) for the rotated, normalised
+// direction `rot`: u = 0.5 + atan2(y, x) / 2pi, v = 0.5 - asin(z) / pi, then
+// `(u * W) as usize % W`, `(v * H) as usize % H`.  sky_index_f64 is that, in f64.
+__device__ __forceinline__ void sky_index_f64(d3 rot, uint32_t W, uint32_t H, uint32_t& x, uint32_t& y) {
+    const double PI = 3.14159265358979323846;
+    double theta = atan2(rot.y, rot.x);
+    double phi = asin(rot.z);
+    double u = 0.5 + theta / (2.0 * PI);
+    double v = 0.5 - phi / PI;
+    x = (uint32_t)(sat_u64(u * (double)W, 18446744073709551616.0, ~0ull) % (uint64_t)W);
+    y = (uint32_t)(sat_u64(v * (double)H, 18446744073709551616.0, ~0ull) % (uint64_t)H);
+}
+// The same indices from f32 angles, certified: U = u*W and V = v*H are evaluated in f32
+// (OCML atan2f; the elevation as atan2f(z, |(x, y)|), which equals asin(z) for a unit
+// vector and is well conditioned at every elevation), and accepted only when both lie
+// farther from a texel boundary (an integer, 0 and W included) than their error bound:
+// |U32 - U| <= W (4 ulp(pi) atan2f + 2^-23 input rounding) / 2pi + the two f32 roundings
+// ~= 2.4e-7 W, |V32 - V| ~= 2.6e-7 H; the margins are 1e-6 W and 2e-6 H (>= 4x), and
+// |(x, y)| >= 1e-4 keeps the f64 asin's own sensitivity at the poles (tan(phi) 2^-53)
+// negligible.  Returns false when undecided (about 0.4% of directions): the caller then
+// runs sky_index_f64.  Decided indices equal sky_index_f64's
+// (tests/test_gpu_device_kat.py: 4M random and near-boundary directions).
+__device__ __forceinline__ bool sky_index_f32(d3 rot, uint32_t W, uint32_t H, uint32_t& x, uint32_t& y) {
+    const float fx = (float)rot.x, fy = (float)rot.y, fz = (float)rot.z;
+    const float r = __builtin_sqrtf(__builtin_fmaf(fx, fx, fy * fy));
+    const float th = atan2f(fy, fx), ph = atan2f(fz, r);
+    const float fW = (float)W, fH = (float)H;
+    const float U = __builtin_fmaf(th, fW * 0.159154943f, fW * 0.5f);
+    const float V = __builtin_fmaf(ph, fH * -0.318309886f, fH * 0.5f);
+    const float iu = __builtin_floorf(U), iv = __builtin_floorf(V);
+    const float du = U - iu, dv = V - iv;
+    const float mu = fW * 1e-6f, mv = fH * 2e-6f;
+    x = (uint32_t)(int32_t)iu;
+    y = (uint32_t)(int32_t)iv;
+    return r >= 1e-4f && du > mu && du < 1.0f - mu && dv > mv && dv < 1.0f - mv && iu >= 0.0f && iu < fW &&
+           iv >= 0.0f && iv < fH;
+}
+
 // Quad::hit acceptance (quad.rs:84-95, plane.rs:20-32), given the plane (normal, D);
 // `tail(Q, u, v, w)` fetches the rest only once the plane hit lies in [tmin, tmax].
 template <class Tail>

@@ -669,20 +669,13 @@ __device__ GS_NOINLINE d3 texture_value(const DevScene& sc, uint32_t tex, double
 // HDRI::sample's texel (camera.rs:257-270) for an already normalised, rotated direction.
 __device__ __forceinline__ d3 hdri_texel(const DevScene& sc, d3 rot, unsigned long long* cnt) {
     const gs_background& bg = sc.bg;
-    const double PI = 3.14159265358979323846;
-    uint64_t x, y;
-    {
-#ifdef GS_ABL_SKY  // ablation build (A/B only, wrong sky): no atan2 / asin
-        double theta = rot.y * 3.0, phi = rot.z;
-#else
-        double theta = atan2(rot.y, rot.x);
-        double phi = asin(rot.z);
+    uint32_t x, y;
+#ifndef GS_SKY_CERT
+#define GS_SKY_CERT 1
 #endif
-        double u = 0.5 + theta / (2.0 * PI);
-        double v = 0.5 - phi / PI;
-        x = sat_u64(u * (double)bg.width, 18446744073709551616.0, ~0ull) % (uint64_t)bg.width;
-        y = sat_u64(v * (double)bg.height, 18446744073709551616.0, ~0ull) % (uint64_t)bg.height;
-    }
+    // f32 angles where they certify the texel, else the reference's f64 atan2 / asin
+    // (sky_index_f32 / sky_index_f64, geometry.hpp)
+    if (!GS_SKY_CERT || !sky_index_f32(rot, bg.width, bg.height, x, y)) sky_index_f64(rot, bg.width, bg.height, x, y);
     const uint64_t k = y * (uint64_t)bg.width + x;
     atomicAdd(&cnt[C_HDRI], 1ull);
     if (sc.hdri_rgbe) {

@@ -115,6 +115,20 @@ __global__ void k_math(int n, int which, const double* x, const double* y, doubl
     out[i] = r;
 }
 
+// The sky texel index: f32 certified (-1, -1 when undecided) and the f64 reference path.
+__global__ void k_sky(int n, uint32_t W, uint32_t H, const double* dir, int* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const d3 r = mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+    uint32_t x = 0, y = 0, x64 = 0, y64 = 0;
+    const bool ok = sky_index_f32(r, W, H, x, y);
+    sky_index_f64(r, W, H, x64, y64);
+    out[4 * i] = ok ? (int)x : -1;
+    out[4 * i + 1] = ok ? (int)y : -1;
+    out[4 * i + 2] = (int)x64;
+    out[4 * i + 3] = (int)y64;
+}
+
 template <class T>
 static T* dcopy(const T* h, size_t n) {
     T* d = nullptr;
@@ -197,6 +211,15 @@ int kat_math(int n, int which, const double* x, const double* y, double* out) {
     hipLaunchKernelGGL(k_math, grid(n), dim3(256), 0, 0, n, which, dx, dy, dout);
     back(out, dout, n);
     (void)hipFree(dx); (void)hipFree(dy);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+int kat_sky(int n, uint32_t W, uint32_t H, const double* dir, int* out) {
+    double* dd = dcopy(dir, 3 * (size_t)n);
+    int* dout = dcopy<int>(nullptr, 4 * (size_t)n);
+    hipLaunchKernelGGL(k_sky, grid(n), dim3(256), 0, 0, n, W, H, dd, dout);
+    back(out, dout, 4 * (size_t)n);
+    (void)hipFree(dd);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 

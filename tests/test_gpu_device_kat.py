@@ -22,7 +22,8 @@ def kat(built):
                     "kat_sphere": [C.c_int, P, P, P, P, P],
                     "kat_tri": [C.c_int, P, P, P, P], "kat_rng": [C.c_int, P, P, P, C.c_int, P],
                     "kat_math": [C.c_int, C.c_int, P, P, P],
-                    "kat_noise": [C.c_int, C.c_int, P, C.c_double, P, P]}.items():
+                    "kat_noise": [C.c_int, C.c_int, P, C.c_double, P, P],
+                    "kat_sky": [C.c_int, C.c_uint32, C.c_uint32, P, P]}.items():
         getattr(L, f).argtypes = args
         getattr(L, f).restype = C.c_int
     return L
@@ -135,6 +136,36 @@ def test_sphere_matches_oracle_bitwise(kat):
         assert (h is not None) == bool(hit[i]), i
         if h is not None:
             assert h["t"] == t[i], i  # sqrt and / are correctly rounded on both sides
+
+
+@pytest.mark.parametrize("W,H", [(1024, 512), (4096, 2048), (7, 3)])
+def test_certified_sky_index_equals_f64(kat, W, H):
+    """sky_index_f32 (f32 atan2f angles, accepted only away from texel boundaries) gives the
+    f64 path's texel column and row whenever it decides, on uniform directions and on
+    directions within 1e-10 .. 1e-4 rad of column and row boundaries, and decides almost
+    all uniform directions."""
+    rng = np.random.default_rng(13)
+    n = 1_000_000
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1)[:, None]
+    k = n // 2
+    # near column boundaries: theta = 2 pi (i / W - 0.5) + delta; near row boundaries:
+    # phi = pi (0.5 - j / H) + delta (the inverse of u, v in HDRI::sample)
+    delta = np.where(rng.random(k) < 0.5, -1, 1) * 10.0 ** rng.uniform(-10, -4, k)
+    th = 2 * np.pi * (rng.integers(0, W + 1, k) / W - 0.5) + delta
+    ph = np.arcsin(np.clip(d[:k, 2], -1, 1))
+    half = k // 2
+    ph[:half] = np.pi * (0.5 - rng.integers(0, H + 1, half) / H) + delta[:half]
+    th[:half] = rng.uniform(-np.pi, np.pi, half)
+    d[:k] = np.stack([np.cos(ph) * np.cos(th), np.cos(ph) * np.sin(th), np.sin(ph)], 1)
+    d = np.ascontiguousarray(d)
+    out = np.zeros((n, 4), np.int32)
+    assert kat.kat_sky(n, W, H, ptr(d), ptr(out)) == 0
+    dec = out[:, 0] >= 0
+    assert np.array_equal(out[dec, :2], out[dec, 2:])
+    # undecided share of uniform directions ~ 2 (1e-6 W + 2e-6 H): 0.4% for the 1024x512 sky
+    assert dec[k:].mean() > 1.0 - 6e-6 * (W + H)
+    assert (~dec[:k]).sum() > 1000  # the boundary cases do reach the f64 path
 
 
 def test_triangle_matches_oracle_bitwise(kat):
