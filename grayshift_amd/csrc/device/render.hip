@@ -168,6 +168,7 @@ struct KArgs {
     uint32_t lds_nodes;  // node records [0, lds_nodes) are mirrored in each block's LDS,
     uint32_t lds_leaves; // then leaf records [0, lds_leaves)
     uint32_t lds_quads;  // then quad records [0, lds_quads)
+    uint32_t lane_nd;    // f64 lane-state fields in LDS: lane_nd(chunked)
 };
 
 enum { S_NEED = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };
@@ -995,8 +996,12 @@ enum { L_ITEM = 0, L_PIX, L_BLEFT, L_SAMPLE, L_DEPTH, L_HINST, L_NI };  // (samp
 #else
 #define GS_STAMP_LDS 0
 #endif
-__host__ __device__ constexpr size_t lane_lds_bytes() {
-    return (size_t)GS_BLOCK * (L_ND * 8 + L_NI * 4) + 128 + GS_STAMP_LDS;
+// Fixed-spp (chunked) launches never reach the stop test, so their lanes keep only the
+// three colour sums: the 24 KiB of Σlum / Σlum² / sample-count slots go to the mirror.
+enum { L_ND_CHUNKED = L_LSUM };
+__host__ __device__ constexpr uint32_t lane_nd(bool chunked) { return chunked ? (uint32_t)L_ND_CHUNKED : (uint32_t)L_ND; }
+__host__ __device__ constexpr size_t lane_lds_bytes(bool chunked) {
+    return (size_t)GS_BLOCK * (lane_nd(chunked) * 8 + L_NI * 4) + 128 + GS_STAMP_LDS;
 }
 
 template <int FEAT>
@@ -1026,7 +1031,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     const QuadSrc qs{s_quads, A.tquads, A.lds_quads};
     // Per-lane pixel / path state after the mirror: [L_ND][GS_BLOCK] f64, [L_NI][GS_BLOCK] u32.
     double* s_d = (double*)(s_quads + (size_t)A.lds_quads * sizeof(TQuad));
-    uint32_t* s_i = (uint32_t*)(s_d + L_ND * GS_BLOCK);
+    uint32_t* s_i = (uint32_t*)(s_d + A.lane_nd * GS_BLOCK);
     unsigned long long* s_cnt = (unsigned long long*)(s_i + L_NI * GS_BLOCK);
 #ifdef GS_STAMPS
     unsigned long long* s_reg = s_cnt + 16;  // [(GS_BLOCK / 64) * 8]
@@ -1274,16 +1279,16 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         LD(L_CSR) = 0.0;
                         LD(L_CSG) = 0.0;
                         LD(L_CSB) = 0.0;
-                        LD(L_LSUM) = 0.0;
-                        LD(L_LSQ) = 0.0;
-                        // first batch starts (camera.rs:137)
-                        LD(L_SCOUNT) = 0.0 + (double)P->ss.batch_size;
                         if (P->chunk) {
                             LI(L_ITEM) = item * cpp + ck;
                             LI(L_SAMPLE) = ck * P->chunk;
                             LI(L_BLEFT) = min(P->chunk, P->ss.batch_size - ck * P->chunk);
                             if (ck == 0) atomicAdd(&s_cnt[C_PIX], 1ull);
                         } else {
+                            LD(L_LSUM) = 0.0;
+                            LD(L_LSQ) = 0.0;
+                            // first batch starts (camera.rs:137)
+                            LD(L_SCOUNT) = 0.0 + (double)P->ss.batch_size;
                             LI(L_ITEM) = item;
                             LI(L_BLEFT) = P->ss.batch_size;
                             LI(L_SAMPLE) = 0u;
@@ -1708,7 +1713,9 @@ static int32_t g_leaf_batch = 12;  // swept on MI355X C4 with leaf runs: 8 -> 45
 static int64_t g_lds_mirror = GS_LDS_MIRROR;
 static int64_t lds_mirror_budget() {
     const int64_t share = (int64_t)160 * 1024 * GS_BLOCK / (GS_MIN_WAVES * 4 * 64);  // the block's share of the CU
-    const int64_t left = share - (int64_t)GS_BLOCK * (L_ND * 8 + L_NI * 4) - 1024;  // 1 KiB: static LDS + slack
+    // (sized for fixed-spp launches; an adaptive launch's larger lane state shrinks the
+    // mirror's prefixes to fit at launch)
+    const int64_t left = share - (int64_t)GS_BLOCK * (L_ND_CHUNKED * 8 + L_NI * 4) - 1024;  // 1 KiB: static LDS + slack
     return left > 0 ? left : 0;
 }
 // -1 auto, 0 never split a pixel's samples.  Swept on MI355X with batched queue claims,
@@ -1765,11 +1772,16 @@ struct gs_device_scene {
     // Launch state, mutated by launches of a const scene: guarded by `mu`.
     std::mutex mu;
     // launch geometry, computed at the first launch (host API queries cost ~0.5 ms each)
-    bool launch_ready = false;
-    int cus = 0, per_cu = 0;
-    uint32_t launch_lds_nodes = 0, launch_lds_leaves = 0, launch_lds_quads = 0;
-    size_t launch_lds = 0;
-    int launch_feat = 0;  // feat, minus GS_FEAT_LDSTREE when the launch mirror is a strict prefix
+    // Launch shape per lane-state layout ([1]: fixed-spp / chunked launches, [0]: adaptive):
+    // the mirror prefixes that fit next to that lane state, the dynamic LDS, the kernel
+    // instantiation (feat minus GS_FEAT_LDSTREE when the mirror is a strict prefix), blocks/CU.
+    struct LaunchCfg {
+        bool ready = false;
+        uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0;
+        size_t lds = 0;
+        int feat = 0, per_cu = 0;
+    } lcfg[2];
+    int cus = 0;
     LaunchSlot slots[kLaunchSlots];
     uint32_t next_slot = 0;
 };
@@ -2507,7 +2519,9 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     a.node_steps = std::max(1, std::min<int32_t>(GS_NODE_STEPS, g_node_steps > 0 ? g_node_steps : ds->node_steps));
     gs_device_scene* mds = const_cast<gs_device_scene*>(ds);
     std::lock_guard<std::mutex> lock(mds->mu);
-    if (!mds->launch_ready) {
+    const bool chunked = kp.chunk != 0;
+    gs_device_scene::LaunchCfg& lc = mds->lcfg[chunked ? 1 : 0];
+    if (!lc.ready) {
         HIPCHK(hipDeviceGetAttribute(&mds->cus, hipDeviceAttributeMultiprocessorCount, dev));
         // The mirror takes what the block's LDS limit leaves after the kernel's static LDS
         // and the lane state (any prefix of either record array is a valid mirror).
@@ -2517,7 +2531,7 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
         HIPCHK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
         // The node mirror must start at LDS address 0 (load_tnode): no static LDS.
         if (fa.sharedSizeBytes != 0) return fail(GS_ERR_UNSUPPORTED, "render kernel with static LDS");
-        const int64_t room = (int64_t)max_lds - (int64_t)lane_lds_bytes();
+        const int64_t room = (int64_t)max_lds - (int64_t)lane_lds_bytes(chunked);
         if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
         uint32_t ln = ds->lds_nodes, ll = ds->lds_leaves, lq = ds->lds_quads;
         auto bytes = [&] {
@@ -2529,24 +2543,24 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
             if (ll) ll = ll - 1 - ll / 16;
             if (lq) lq = lq - 1 - lq / 16;
         }
-        mds->launch_lds_nodes = ln;
-        mds->launch_lds_leaves = ll;
-        mds->launch_lds_quads = lq;
-        mds->launch_lds = lane_lds_bytes() + (size_t)bytes();
-        mds->launch_feat = ds->feat;
-        if (ln < ds->node_records || ll < ds->leaf_records) mds->launch_feat &= ~GS_FEAT_LDSTREE;
+        lc.lds_nodes = ln;
+        lc.lds_leaves = ll;
+        lc.lds_quads = lq;
+        lc.lds = lane_lds_bytes(chunked) + (size_t)bytes();
+        lc.feat = ds->feat;
+        if (ln < ds->node_records || ll < ds->leaf_records) lc.feat &= ~GS_FEAT_LDSTREE;
         int occ = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel_for(mds->launch_feat), GS_BLOCK,
-                                                            mds->launch_lds));
-        mds->per_cu = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
-        mds->launch_ready = true;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel_for(lc.feat), GS_BLOCK, lc.lds));
+        lc.per_cu = occ < 1 ? 1 : (occ > 8 ? 8 : occ);
+        lc.ready = true;
     }
     const int cus = ds->cus;
-    const size_t lds = ds->launch_lds;
-    a.lds_nodes = ds->launch_lds_nodes;
-    a.lds_leaves = ds->launch_lds_leaves;
-    a.lds_quads = ds->launch_lds_quads;
-    const int per_cu = g_blocks_per_cu > 0 ? g_blocks_per_cu : ds->per_cu;
+    const size_t lds = lc.lds;
+    a.lds_nodes = lc.lds_nodes;
+    a.lds_leaves = lc.lds_leaves;
+    a.lds_quads = lc.lds_quads;
+    a.lane_nd = lane_nd(chunked);
+    const int per_cu = g_blocks_per_cu > 0 ? g_blocks_per_cu : lc.per_cu;
     int64_t blocks = (int64_t)cus * per_cu;
     // no more waves than work: one lane per item at most
     int64_t max_blocks = ((int64_t)kp.n_items + GS_BLOCK - 1) / GS_BLOCK;
@@ -2583,7 +2597,7 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     hipLaunchKernelGGL(gs_params_kernel, dim3(1), dim3(64), 0, st, kp, sl.params);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(sl.queue, 0, 4, st));
-    hipLaunchKernelGGL(kernel_for(ds->launch_feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
+    hipLaunchKernelGGL(kernel_for(lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
     if (chunk) {
         const unsigned grid = (unsigned)std::min<int64_t>((cap + 255) / 256, 8192);
