@@ -171,7 +171,9 @@ struct KArgs {
     uint32_t lane_nd;    // f64 lane-state fields in LDS: lane_nd(chunked)
 };
 
-enum { S_NEED = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3 };
+// S_CAM: the lane's next sample needs its camera ray (set by the refill for a new item and
+// by the shade pass for a finished sample; one advance() at the loop head serves both).
+enum { S_NEED = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3, S_CAM = 4 };
 
 // Device-side refs in the two-child node records of BVHs under instances (nested_bvh):
 // a BVH node is its bare index (< 2^26), leaves keep their ABI tag (kind >= 2 in the top
@@ -1102,24 +1104,29 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 
     // Start samples until one needs tracing or the pixel is finished:
     // leaves st = S_TRACE (ray ready) or S_NEED (pixel written).
+    // End of a chunk: its Σrgb, summed per pixel by gs_combine_kernel.
+    auto end_chunk = [&]() {
+        const uint32_t item = LI(L_ITEM);
+        double* o = P->partial + (size_t)item * 3;
+        o[0] = LD(L_CSR);
+        o[1] = LD(L_CSG);
+        o[2] = LD(L_CSB);
+#ifndef GS_STAMPS
+        if (P->item_visits) atomicAdd(&P->item_visits[item / P->cpp], c_nodes);
+#endif
+        atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
+        atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
+        c_nodes = 0;
+        c_sph = 0;
+        st = S_NEED;
+    };
+
     auto advance = [&]() {
 #pragma unroll 1
         for (;;) {
             if (LI(L_BLEFT) == 0) {
-                if (P->chunk) {  // end of a chunk: its Σrgb, summed per pixel by gs_combine_kernel
-                    const uint32_t item = LI(L_ITEM);
-                    double* o = P->partial + (size_t)item * 3;
-                    o[0] = LD(L_CSR);
-                    o[1] = LD(L_CSG);
-                    o[2] = LD(L_CSB);
-#ifndef GS_STAMPS
-                    if (P->item_visits) atomicAdd(&P->item_visits[item / P->cpp], c_nodes);
-#endif
-                    atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
-                    atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
-                    c_nodes = 0;
-                    c_sph = 0;
-                    st = S_NEED;
+                if (P->chunk) {
+                    end_chunk();
                     return;
                 }
                 // end of a batch (camera.rs:149-164)
@@ -1205,6 +1212,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     for (;;) {
         // ---------------------------------------------------------- refill
         GS_STAMP(ts0);
+        // Refill and camera rays: lanes without an item take one (S_NEED -> S_CAM), then every
+        // lane whose next sample needs a camera ray -- a new item's first, or the next sample
+        // after the shade pass finished one -- runs advance() together, once per loop
+        // iteration (the wave pays for get_ray once, not once per refill and once per shade).
+        // advance() hands back S_TRACE, or S_NEED when an item ends there (adaptive settings,
+        // max_depth 0), which sends the lane round once more.
+#pragma unroll 1
+        for (;;) {
         uint64_t need = __builtin_amdgcn_ballot_w64(st == S_NEED);
 #pragma unroll 1
         while (need != 0 && !qdone) {
@@ -1293,13 +1308,20 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                             LI(L_BLEFT) = P->ss.batch_size;
                             LI(L_SAMPLE) = 0u;
                         }
-                        advance();
+                        st = S_CAM;
                     }
                 }
             }
             need = __builtin_amdgcn_ballot_w64(st == S_NEED);
         }
-        if (fresh) {
+        if (st == S_CAM) {
+            GS_MARK("adv_begin");
+            advance();
+            GS_MARK("adv_end");
+        }
+        if (qdone || __builtin_amdgcn_ballot_w64(st == S_NEED) == 0) break;
+        }
+        if (fresh) {  // scattered rays (shade pass) and camera rays together
             begin_ray();
             fresh = false;
         }
@@ -1580,25 +1602,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                 }
             }
-            if (ends) {
+            if (ends) {  // the sample is done; its item's next camera ray comes at the loop head
                 GS_STAMP(r0);
-                GS_MARK("adv_begin");
                 add_sample(Lr, Lg, Lb);
-                advance();
-                GS_MARK("adv_end");
+                if (P->chunk && LI(L_BLEFT) == 0) end_chunk();  // -> S_NEED
+                else st = S_CAM;
                 GS_REGION(4, r0);
             }
-        }
-        if (fresh) {  // scattered and new camera rays together
-#ifdef GS_STAMPS
-            uint64_t r0;
-#endif
-            GS_STAMP(r0);
-            GS_MARK("br_begin");
-            begin_ray();
-            GS_MARK("br_end");
-            GS_REGION(3, r0);
-            fresh = false;
         }
 #ifdef GS_STAMPS
         GS_STAMP(ts3);

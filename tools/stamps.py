@@ -47,7 +47,8 @@ def main():
     # staged shading (GS_FEAT_MIXED, media, nested) stamps all of it as region 2
     print("shade regions (%% of shade clock): " + "  ".join(
         "%s %.1f%%" % (n, 100.0 * x / max(1, v[2])) for n, x in
-        zip(["background", "reconstruct", "scatter (staged: all shading)", "begin_ray", "sample+advance"], reg)))
+        zip(["background", "reconstruct", "scatter (staged: all shading)", "-", "add_sample + chunk end"], reg)))
+    # camera rays (advance) and begin_ray run at the loop head since r02: inside "refill"
 
 
 if __name__ == "__main__":
