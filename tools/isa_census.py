@@ -3,7 +3,7 @@
 
 Compiles render.hip for gfx950 with -DGS_ISA_MARKS (assembler comments delimit the
 regions; everything else is the product build's flags), extracts one kernel
-instantiation (default FEAT=4: the C4 kernel) and counts instructions by class:
+instantiation (default FEAT=20: the C4 kernel, leaf runs + staged shading) and counts instructions by class:
 
 * loop head: from the traversal loop's header label to the node-pass mark (ballots,
   shade-count and pass-kind tests, shared by both passes);
@@ -62,7 +62,7 @@ def census(lines):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--feat", type=int, default=4)
+    ap.add_argument("--feat", type=int, default=20)
     ap.add_argument("--dump", default=None, help="write the marked regions' assembly here")
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as d:
