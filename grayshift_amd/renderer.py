@@ -120,7 +120,10 @@ class HostScene:
             self.handle = None
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001  (interpreter shutdown: the binding may be gone)
+            pass
 
     def stats(self):
         f = self.flat
@@ -233,4 +236,7 @@ class Renderer:
             self.host.close()
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001  (interpreter shutdown: the binding may be gone)
+            pass

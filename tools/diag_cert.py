@@ -9,7 +9,13 @@ import grayshift_amd as g
 from grayshift_amd import _native as N, scenes
 from grayshift_amd.scene import fixed_spp
 name = sys.argv[1] if len(sys.argv) > 1 else "final_scene"
-sc = scenes.SCENES[name](width=40, settings=fixed_spp(8))
+# a BASELINE config at its full size and spp (or width / spp given after it), else a scene
+# at 40 px, 8 spp
+if name in scenes.CONFIGS:
+    kw = {"width": int(sys.argv[2]), "spp": int(sys.argv[3])} if len(sys.argv) > 3 else {}
+    sc = scenes.config(name, **kw)
+else:
+    sc = scenes.SCENES[name](width=40, settings=fixed_spp(8))
 r = g.Renderer(sc)
 dev = torch.device("cuda", 0)
 packed = torch.zeros(r.capacity * 3, dtype=torch.float32, device=dev)
