@@ -4,21 +4,31 @@
 Contract:
     python bench.py --gpus N --steps K --warmup W
 One step = one full frame of the configured workload (default C4: the 10k-sphere
-BVH scene, 1920x1080, 512 spp, HDRI sky), tile-partitioned over the N ranks (64x64
-tiles; cost-balanced plan computed on rank 0 and broadcast), then one RCCL gather of
-the finished tiles to rank 0 and an unpack into the frame.  The scene is resident in
-HBM before timing starts.  value = all rays traced by all ranks / wall time (max over
-ranks); a "ray" is one world.hit call (camera.rs:177), counted on the device by the very
-launches timed.
+BVH scene, 1920x1080, 512 spp, HDRI sky), tile-partitioned over N GPUs (64x64 tiles;
+cost-balanced plan for N > 1), then one RCCL gather of the finished tiles to the first
+GPU and an unpack into the frame.  The scene is resident in HBM before timing starts.
+value = all rays traced on all GPUs / wall time; a "ray" is one world.hit call
+(camera.rs:177), counted on the device by the very launches timed.
+
+Two launch modes, one frame:
+* no launcher (WORLD_SIZE unset): one process drives N devices through the C-ABI frame
+  context (gs_multi_create once — scene upload, ncclCommInitAll — then gs_multi_render
+  per frame: render on every device, ncclGather, unpack).  --gpus N above the visible
+  device count fails with a message and a non-zero exit.
+* under torch.distributed.run (WORLD_SIZE = N): one process per GPU; each rank renders
+  its planned tiles (plan from rank 0, broadcast), one torch.distributed gather (backend
+  nccl = RCCL over xGMI) to rank 0, which unpacks; the time is the max over ranks.
 
 Rank 0 prints ONE JSON line with, beside the contract's fields:
 * parity — the timed frame checked against the CPU oracle (the reference's algorithm
   restated, oracle/) on a deterministic pixel subset, at the full config;
 * cpu_baseline — at N=1 the oracle's render time on that subset (median of 3, world and
   BVH build excluded), on this host's cores;
-* roofline — the kernel's binding ceiling, VALU issue, from the PMC summary of this very
-  code object (profiles/pmc/, keyed by the hash of the library's gfx950 code objects),
-  with the measured HBM fraction and the cache-served algorithmic byte rate beside it.
+* roofline — the kernel's binding ceiling, VALU issue: every VALU instruction class of the
+  PMC summary of this very code object (profiles/pmc/, keyed by the hash of the library's
+  gfx950 code objects) priced at its measured issue cycles (VALU_CYCLES), over the SIMDs'
+  cycles of this run's kernel time; the measured HBM fraction and the cache-served
+  algorithmic byte rate beside it.
 """
 import argparse
 import json
@@ -38,7 +48,16 @@ BYTES = {"node_visits": 56, "sphere_tests": 40, "msphere_tests": 64, "quad_tests
          "noise_evals": 168}  # noise: 7 octaves x 8 corners x 3 permutation-table bytes
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SIMDS = 1024  # 256 CUs x 4 SIMDs
-VALU_ISSUE_CYCLES = 4  # cycles per wave64 VALU instruction of one wave (f64: half-rate SIMD-32)
+# Issue cycles per wave64 VALU instruction on one SIMD-32 at full occupancy, by the PMC
+# instruction classes (SQ_INSTS_VALU_*; "OTHER" = SQ_INSTS_VALU minus the listed classes:
+# moves, compares, selects, bit operations, f32 min/max).  MI355X_MICROARCH.md:54,473: a
+# wave64 32-bit VALU instruction issues over 2 cycles on a SIMD-32.  The rest measured by
+# tools/ubench/valu_rate.hip (profiles/r03/valu_rate_ubench.txt: 8 waves/SIMD, SGPR /
+# inline-constant operands, cycles at the in-kernel clock): f64 add / mul / fma and the
+# 64-bit integer ops issue like 32-bit ones; f64 transcendentals (v_sqrt_f64, v_rcp_f64)
+# take 8, f32 ones 2.
+VALU_CYCLES = {"ADD_F32": 2, "MUL_F32": 2, "FMA_F32": 2, "TRANS_F32": 2, "ADD_F64": 2, "MUL_F64": 2,
+               "FMA_F64": 2, "TRANS_F64": 8, "INT32": 2, "INT64": 2, "CVT": 2, "OTHER": 2}
 PARITY_TOL = 1e-3  # north star: per-channel |delta| < 1e-3 vs the CPU path at a fixed seed
 
 
@@ -85,15 +104,75 @@ def parse():
 
 def main():
     a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in os.environ and world != a.gpus:
+        raise SystemExit("bench.py: --gpus %d under a launcher with WORLD_SIZE=%d (one rank per GPU)" % (a.gpus, world))
+    if world > 1 or a.gather:
+        return main_ranks(a, world)
+    return main_context(a)
+
+
+def load_scene(a):
+    import grayshift_amd as g
+    from grayshift_amd import scenes
+    g.set_tuning(a.shade_batch or 52, a.blocks_per_cu or 0, 12 if a.leaf_batch is None else a.leaf_batch,
+                 -1 if a.sample_chunk is None else a.sample_chunk)
+    g._native.check(g._native.lib.gs_set_node_steps(a.node_steps))
+    if a.config in scenes.CONFIGS:
+        return scenes.config(a.config, width=a.width, spp=a.spp)
+    a.width, a.spp = a.width or 400, a.spp or 64
+    return scenes.SCENES[a.config](width=a.width, settings=scenes.fixed_spp(a.spp))
+
+
+def main_context(a):
+    """One process, N devices, through the C-ABI frame context (gs_multi_*)."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    n_vis = torch.cuda.device_count()  # (counts devices without initialising HIP)
+    if a.gpus < 1 or a.gpus > n_vis:
+        print("bench.py: --gpus %d but %d GPU(s) visible" % (a.gpus, n_vis), file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    import grayshift_amd as g
+    from grayshift_amd import _native as N
+    sc = load_scene(a)
+    plan = a.gpus > 1 and not a.no_plan
+    m = g.MultiRenderer(sc, num_gpus=a.gpus, tile=a.tile, plan=plan)
+
+    def sync_all():
+        for d in m.devices:
+            torch.cuda.synchronize(d)
+
+    for _ in range(a.warmup):
+        m.render(seed=a.seed)
+    sync_all()
+    kms, tot = [], None
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        r = m.render(seed=a.seed)  # synchronous: returns once the frame is unpacked
+        kms.append(r["stats"]["kernel_ms_max"])
+        tot = r["counters"] if tot is None else {k: tot[k] + v for k, v in r["counters"].items()}
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    c = {k: v // a.steps for k, v in tot.items()}
+    d_rgb, dev0 = m.frame_ptr()
+    img = np.zeros((m.height, m.width, 3), dtype=np.float32)
+    N.check(N.lib.gs_device_download(img.ctypes.data, C.c_void_p(d_rgb), img.nbytes))
+    emit(a, sc, m, c, elapsed, sum(kms) / len(kms), img, a.gpus,
+         {"tile_plan": "cost-balanced" if plan else "round-robin",
+          "collective": "rccl" if a.gpus > 1 else "none",
+          "launch": "one process, %d device(s): gs_multi_create once, gs_multi_render per frame" % a.gpus})
+    m.close()
+
+
+def main_ranks(a, world):
+    """One process per GPU under torch.distributed.run (or --gather at N=1)."""
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and world == 1 and a.gpus > 1:
-        raise SystemExit("--gpus %d needs torch.distributed.run with %d ranks" % (a.gpus, a.gpus))
     if a.share_gpu:
         local = 0
     if local >= torch.cuda.device_count():
@@ -101,32 +180,20 @@ def main():
                          % (rank, local, torch.cuda.device_count()))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    use_pg = world > 1 or a.gather
-    if use_pg:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29511")
-        if a.backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-        else:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
-    host_coll = use_pg and a.backend == "gloo"  # gloo collectives on host copies
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    if a.backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    host_coll = a.backend == "gloo"  # gloo collectives on host copies
 
     import grayshift_amd as g
-    from grayshift_amd import scenes
-
-    g.set_tuning(a.shade_batch or 52, a.blocks_per_cu or 0, 12 if a.leaf_batch is None else a.leaf_batch,
-                 -1 if a.sample_chunk is None else a.sample_chunk)
-    g._native.check(g._native.lib.gs_set_node_steps(a.node_steps))
-    if a.config in scenes.CONFIGS:
-        sc = scenes.config(a.config, width=a.width, spp=a.spp)
-    else:
-        a.width, a.spp = a.width or 400, a.spp or 64
-        sc = scenes.SCENES[a.config](width=a.width, settings=scenes.fixed_spp(a.spp))
+    sc = load_scene(a)
     # N > 1: tiles are assigned by a cost-balanced plan (a 1-spp pilot of the frame),
     # computed once at setup on rank 0 and broadcast, so every rank uses the same one
     # (outside the timed region, like the BVH build).
     plan = world > 1 and not a.no_plan
-    order = None
     if plan:
         cam = g.camera(sc.camera)
         tiles = -(-cam.image_width // a.tile) * -(-cam.image_height // a.tile)
@@ -148,7 +215,7 @@ def main():
     packed = torch.zeros(cap0 * 3, dtype=torch.float32, device=dev)
     counters = torch.zeros(16, dtype=torch.int64, device=dev)
     frame = torch.zeros(r.height * r.width * 3, dtype=torch.float32, device=dev) if rank == 0 else None
-    gathered = torch.empty(world * cap0 * 3, dtype=torch.float32, device=dev) if (rank == 0 and use_pg) else None
+    gathered = torch.empty(world * cap0 * 3, dtype=torch.float32, device=dev) if rank == 0 else None
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
@@ -170,14 +237,12 @@ def main():
                 r.unpack_async(gathered.data_ptr(), frame.data_ptr(), world, sptr)
             else:
                 dist.gather(src, dst=0)
-        elif use_pg:  # RCCL over xGMI
+        else:  # RCCL over xGMI
             if rank == 0:
                 dist.gather(packed, gather_list=list(gathered.view(world, -1).unbind(0)), dst=0)
                 r.unpack_async(gathered.data_ptr(), frame.data_ptr(), world, sptr)
             else:
                 dist.gather(packed, dst=0)
-        else:
-            r.unpack_async(packed.data_ptr(), frame.data_ptr(), 1, sptr)
         if timed:
             kernel_ms.append((ev0, ev1))
 
@@ -189,95 +254,116 @@ def main():
         tot += counters
     torch.cuda.synchronize()
     tot.zero_()
-    if use_pg:
-        dist.barrier()
+    dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step(True)
         tot += counters
     torch.cuda.synchronize()
-    if use_pg:
-        dist.barrier()
+    dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kms = [e0.elapsed_time(e1) for e0, e1 in kernel_ms]
-    if use_pg:
-        cdev = torch.device("cpu") if host_coll else dev
-        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        tot_c = tot.to(cdev)
-        dist.all_reduce(tot_c, op=dist.ReduceOp.SUM)
-        tot = tot_c.to(dev)
-        km = torch.tensor([sum(kms) / len(kms)], dtype=torch.float64, device=cdev)
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
-        kernel_avg_ms = float(km.item())
-    else:
-        kernel_avg_ms = sum(kms) / len(kms)
+    cdev = torch.device("cpu") if host_coll else dev
+    t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    tot_c = tot.to(cdev)
+    dist.all_reduce(tot_c, op=dist.ReduceOp.SUM)
+    tot = tot_c.to(dev)
+    km = torch.tensor([sum(kms) / len(kms)], dtype=torch.float64, device=cdev)
+    dist.all_reduce(km, op=dist.ReduceOp.MAX)
+    kernel_avg_ms = float(km.item())
 
     from grayshift_amd._native import COUNTER_NAMES
     c = {n: int(tot[i].item()) // a.steps for i, n in enumerate(COUNTER_NAMES)}
-    rays_per_frame = c["rays"]
-    value = rays_per_frame * a.steps / elapsed / 1e6
-
     if rank == 0:
         img = frame.view(r.height, r.width, 3).cpu().numpy()
-        if a.dump:
-            np.save(a.dump, img)
-        cpu = parity = None
-        if not a.no_cpu:
-            stride = a.cpu_stride if world == 1 else a.parity_stride
-            cpu, parity = cpu_check(sc, a, img, stride, runs=a.cpu_runs if world == 1 else 1)
-            if world > 1:
-                cpu = None  # the CPU baseline is an N=1 figure
-        invalid = a.width is not None or a.spp is not None
-        out = {
-            "metric": "Msamples/sec (primary+secondary rays)",
-            "value": round(value, 3),
-            "unit": "Msamples/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (deterministic scene generator, seed 'grayshif'; decoded reference assets)",
-            "config": {
-                "workload": "%s: %s %dx%d, %d spp%s" % (a.config, sc.name, r.width, r.height,
-                                                      sc.settings.batch_size,
-                                                      " (OVERRIDDEN: not the metric)" if invalid else ""),
-                "tile": a.tile, "parallelism": "tiles%d" % world,
-                "tile_plan": "cost-balanced" if plan else "round-robin",
-                "collective": ("rccl" if a.backend == "nccl" else "gloo") if use_pg else "none",
-                "seed": a.seed,
-                "rays_per_frame": rays_per_frame, "paths_per_frame": c["paths"],
-                "node_visits_per_ray": round(c["node_visits"] / max(1, rays_per_frame), 3),
-                "scene": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.scene_info().items()},
-            },
-            "roofline": roofline(a, c, world, kernel_avg_ms, invalid),
-            "parity": parity,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(out), flush=True)
-    if use_pg:
-        dist.destroy_process_group()
+        emit(a, sc, r, c, elapsed, kernel_avg_ms, img, world,
+             {"tile_plan": "cost-balanced" if plan else "round-robin",
+              "collective": "rccl" if a.backend == "nccl" else "gloo",
+              "launch": "torch.distributed.run: %d process(es), one GPU each" % world})
+    dist.destroy_process_group()
     r.close()
+
+
+def emit(a, sc, r, c, elapsed, kernel_avg_ms, img, world, launch_info):
+    """Rank 0's JSON line (kernel_avg_ms: the render launch of the slowest GPU, per frame)."""
+    import numpy as np
+    rays_per_frame = c["rays"]
+    value = rays_per_frame * a.steps / elapsed / 1e6
+    if a.dump:
+        np.save(a.dump, img)
+    cpu = parity = None
+    if not a.no_cpu:
+        stride = a.cpu_stride if world == 1 else a.parity_stride
+        cpu, parity = cpu_check(sc, a, img, stride, runs=a.cpu_runs if world == 1 else 1)
+        if world > 1:
+            cpu = None  # the CPU baseline is an N=1 figure
+    invalid = a.width is not None or a.spp is not None
+    info = r.scene_info() if hasattr(r, "scene_info") else None
+    cfg = {
+        "workload": "%s: %s %dx%d, %d spp%s" % (a.config, sc.name, r.width, r.height, sc.settings.batch_size,
+                                              " (OVERRIDDEN: not the metric)" if invalid else ""),
+        "tile": a.tile, "parallelism": "tiles%d" % world,
+    }
+    cfg.update(launch_info)
+    cfg.update({"seed": a.seed, "rays_per_frame": rays_per_frame, "paths_per_frame": c["paths"],
+                "node_visits_per_ray": round(c["node_visits"] / max(1, rays_per_frame), 3)})
+    if info:
+        cfg["scene"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in info.items()}
+    out = {
+        "metric": "Msamples/sec (primary+secondary rays)",
+        "value": round(value, 3),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (deterministic scene generator, seed 'grayshif'; decoded reference assets)",
+        "config": cfg,
+        "roofline": roofline(a, c, world, kernel_avg_ms, invalid),
+        "parity": parity,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+
+
+def valu_cycles(k):
+    """Issue cycles of a launch's VALU instructions on their SIMDs: every PMC instruction
+    class times its measured cost (VALU_CYCLES), the unclassified rest at 2 cycles.
+    Returns (cycles, {class: [count, cycles]})."""
+    classes = [c for c in VALU_CYCLES if c != "OTHER"]
+    mix = {}
+    listed = 0.0
+    for c in classes:
+        n = float(k.get("SQ_INSTS_VALU_" + c, 0.0))
+        listed += n
+        mix[c] = [n, n * VALU_CYCLES[c]]
+    other = max(0.0, float(k["SQ_INSTS_VALU"]) - listed)
+    mix["OTHER"] = [other, other * VALU_CYCLES["OTHER"]]
+    return sum(v[1] for v in mix.values()), mix
 
 
 def roofline(a, c, world, kernel_ms, invalid):
     """The dominant kernel's ceiling.  The C4 working set (~3.5 MB: threaded BVH records
     and the RGBE sky) lives in LDS / L1 / L2, so HBM does not bound it (measured fabric
-    traffic below); VALU issue does.  frac = VALU wave-instructions x 4 cycles over the
-    SIMDs' cycles, from the PMC summary of this very code object (same config), with the
-    instruction rate taken over this run's kernel time."""
+    traffic below); VALU issue does.  frac = the launch's VALU issue cycles (each PMC
+    instruction class at its measured cycles per wave-instruction on a SIMD-32, VALU_CYCLES)
+    over the SIMDs' cycles of this run's kernel time at the profiled effective clock, from
+    the PMC summary of this very code object (same config).  What the rest of the SIMD
+    time goes to is reported beside it: waves parked on s_waitcnt (SQ_WAIT_ANY) and
+    issue-stalled (SQ_WAIT_INST_ANY) as shares of wave cycles."""
     from grayshift_amd import codeobj
     from grayshift_amd._native import LIB_PATH
     kernel_s = kernel_ms / 1e3
     abytes = algorithmic_bytes(c) / max(1, world)  # per launch (per rank)
-    out = {"bound": "valu_issue", "achieved": None, "peak": None, "unit": "G VALU wave-instr/s", "frac": None,
+    out = {"bound": "valu_issue", "achieved": None, "peak": None, "unit": "G VALU issue-cycles/s", "frac": None,
            "traffic": None, "hbm_frac": None, "kernel_ms": round(kernel_ms, 3),
            "cache_served_algorithmic_GBps": round(abytes / kernel_s / 1e9, 1),
            "cache_served_algorithmic_over_hbm_peak": round(abytes / kernel_s / 1e9 / HBM_PEAK_GBS, 4),
@@ -298,14 +384,19 @@ def roofline(a, c, world, kernel_ms, invalid):
     k = pj["counters"]
     prof_s = pj["kernel_duration_ms_profiled"] / 1e3
     clock = k["GRBM_GUI_ACTIVE"] / 8.0 / prof_s  # effective shader clock of the profiled launch (Hz)
-    achieved = k["SQ_INSTS_VALU"] / kernel_s
-    peak = SIMDS * clock / VALU_ISSUE_CYCLES
+    cyc, mix = valu_cycles(k)
+    achieved = cyc / kernel_s  # VALU issue cycles per second, all SIMDs
+    peak = SIMDS * clock
+    wc = float(k.get("SQ_WAVE_CYCLES", 0.0)) or 1.0
     out.update({"achieved": round(achieved / 1e9, 2), "peak": round(peak / 1e9, 2), "frac": round(achieved / peak, 4),
                 "traffic": pj["hbm_bytes_per_launch"],
                 "hbm_frac": round(pj["hbm_bytes_per_launch"] / kernel_s / 1e9 / HBM_PEAK_GBS, 5),
                 "effective_clock_ghz": round(clock / 1e9, 3),
-                "valu_busy_frac_pmc": round(k["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * k["GRBM_GUI_ACTIVE"] / 8.0), 4)
-                if "SQ_ACTIVE_INST_VALU" in k else None,
+                "valu_instructions": int(k["SQ_INSTS_VALU"]),
+                "valu_cycle_mix": {c2: round(v[1] / cyc, 4) for c2, v in mix.items()},
+                "wave_cycles_waiting": round(float(k.get("SQ_WAIT_ANY", 0.0)) / wc, 4),
+                "wave_cycles_issue_stalled": round(float(k.get("SQ_WAIT_INST_ANY", 0.0)) / wc, 4),
+                "wave_cycles_issuing": round(float(k.get("SQ_ACTIVE_INST_ANY", 0.0)) / wc, 4),
                 "pmc": os.path.relpath(path, ROOT)})
     return out
 

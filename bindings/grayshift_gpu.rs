@@ -25,7 +25,7 @@ pub const GS_REF_TRIANGLE: u32 = 5;
 pub const GS_REF_LIST: u32 = 6;
 pub const GS_REF_INSTANCE: u32 = 7;
 pub const GS_REF_MEDIUM: u32 = 8;
-pub const GS_ABI_VERSION: i32 = 5;
+pub const GS_ABI_VERSION: i32 = 6;
 pub const fn gs_make_ref(kind: u32, idx: u32) -> u32 { (kind << GS_REF_SHIFT) | (idx & 0x0FFF_FFFF) }
 
 #[repr(C)] #[derive(Clone, Copy, Default)]
@@ -122,12 +122,16 @@ pub struct gs_multi_outputs {
     pub rgb: *mut f32, pub rgb8: *mut u8, pub ppm_text: *mut c_char, pub ppm_capacity: i64, pub ppm_len: *mut i64,
 }
 
-/// What one gs_render_multi call did (ABI 4).
+/// What one frame did (SURVEY.md §5 metrics): every synchronous render call fills it (ABI 6).
 #[repr(C)] #[derive(Clone, Copy, Default)]
 pub struct gs_stats {
     pub counters: gs_counters, pub setup_ms: f64, pub total_ms: f64, pub render_ms_max: f64, pub render_ms_min: f64,
     pub gather_ms: f64, pub algorithmic_bytes: u64, pub gathered_bytes: u64, pub num_gpus: i32, pub pad: i32,
+    pub kernel_ms_max: f64, pub kernel_ms_min: f64,
 }
+
+/// The persistent N-GPU frame context (ABI 6, opaque).
+#[repr(C)] pub struct gs_multi { _private: [u8; 0] }
 
 /// What gs_device_scene_create built (ABI 5).
 #[repr(C)] #[derive(Clone, Copy, Default)]
@@ -171,6 +175,7 @@ extern "C" {
     pub fn gs_device_alloc(bytes: i64, d_out: *mut *mut c_void) -> gs_status;
     pub fn gs_device_free(d_ptr: *mut c_void) -> gs_status;
     pub fn gs_device_upload(d_dst: *mut c_void, host_src: *const c_void, bytes: i64) -> gs_status;
+    pub fn gs_device_download(host_dst: *mut c_void, d_src: *const c_void, bytes: i64) -> gs_status;
     pub fn gs_ppm_max_bytes(width: i32, height: i32) -> i64;
     pub fn gs_ppm_scratch_bytes(width: i32, height: i32) -> i64;
     pub fn gs_ppm_encode_async(d_rgb8: *const u8, width: i32, height: i32, d_text: *mut c_char, text_capacity: i64,
@@ -179,15 +184,25 @@ extern "C" {
     /// The whole of camera.rs:100-121 past the world build: PPM text into `out_text`.
     pub fn gs_render_ppm(scene: *const gs_flat_scene, cam: *const gs_camera, ss: *const gs_sample_settings, seed: u64,
                          out_text: *mut c_char, text_capacity: i64, out_len: *mut i64,
-                         counters: *mut gs_counters) -> gs_status;
+                         stats: *mut gs_stats) -> gs_status;
     /// The one-call replacement of camera.rs:105-114.
     pub fn gs_render(scene: *const gs_flat_scene, cam: *const gs_camera, ss: *const gs_sample_settings, seed: u64,
-                     out_rgb: *mut f32, counters: *mut gs_counters) -> gs_status;
+                     out_rgb: *mut f32, stats: *mut gs_stats) -> gs_status;
     /// camera.rs:105-114 (and, with ppm_text, :100-121) on the GPUs of one node, one RCCL gather.
     pub fn gs_render_multi(scene: *const gs_flat_scene, cam: *const gs_camera, ss: *const gs_sample_settings,
                            seed: u64, launch: *const gs_launch, out: *const gs_multi_outputs,
                            stats: *mut gs_stats) -> gs_status;
     pub fn gs_rccl_library() -> *const c_char;
+    /// The persistent N-GPU context (ABI 6): upload + communicator once, then frames.
+    pub fn gs_multi_create(scene: *const gs_flat_scene, launch: *const gs_launch, out: *mut *mut gs_multi) -> gs_status;
+    pub fn gs_multi_render(m: *mut gs_multi, cam: *const gs_camera, ss: *const gs_sample_settings, seed: u64,
+                           out: *const gs_multi_outputs, stats: *mut gs_stats) -> gs_status;
+    pub fn gs_multi_frame(m: *const gs_multi, d_rgb: *mut *const f32, d_rgb8: *mut *const u8,
+                          device: *mut i32) -> gs_status;
+    pub fn gs_multi_devices(m: *const gs_multi, num_gpus: *mut i32, devices: *mut i32, capacity: i32) -> gs_status;
+    pub fn gs_multi_scene(m: *const gs_multi, rank: i32, scene: *mut *const gs_device_scene) -> gs_status;
+    pub fn gs_multi_destroy(m: *mut gs_multi) -> gs_status;
+    pub fn gs_debug_set_multi_collective(always: i32) -> gs_status;
 }
 
 pub fn last_error() -> String {
@@ -198,16 +213,46 @@ pub fn last_error() -> String {
 /// device-formatted PPM text with one call.  `flat`, `cam` and `ss` come from the
 /// crate's `flatten` trait method and `Camera::new`.
 pub fn render_ppm(flat: &gs_flat_scene, cam: &gs_camera, ss: &gs_sample_settings, seed: u64,
-                  out: &mut impl std::io::Write) -> std::io::Result<()> {
+                  out: &mut impl std::io::Write) -> std::io::Result<gs_stats> {
     let cap = unsafe { gs_ppm_max_bytes(cam.image_width, cam.image_height) };
     if cap < 0 { return Err(std::io::Error::new(std::io::ErrorKind::InvalidInput, "bad image size")); }
     let mut text = vec![0u8; cap as usize];
     let mut len: i64 = 0;
-    let st = unsafe {
-        gs_render_ppm(flat, cam, ss, seed, text.as_mut_ptr() as *mut c_char, cap, &mut len, std::ptr::null_mut())
-    };
+    let mut stats = gs_stats::default();
+    let st = unsafe { gs_render_ppm(flat, cam, ss, seed, text.as_mut_ptr() as *mut c_char, cap, &mut len, &mut stats) };
     if st != GS_OK { return Err(std::io::Error::new(std::io::ErrorKind::Other, last_error())); }
-    out.write_all(&text[..len as usize])
+    out.write_all(&text[..len as usize])?;
+    Ok(stats)
+}
+
+/// Many frames of one world on `num_gpus` GPUs (an animation, a benchmark): the scene
+/// upload and the RCCL communicator happen once in `new`, each `frame` is one call.
+pub struct Frames { ctx: *mut gs_multi }
+
+impl Frames {
+    pub fn new(flat: &gs_flat_scene, num_gpus: i32) -> std::io::Result<Frames> {
+        let launch = gs_launch { num_gpus, tile_w: 64, tile_h: 64, plan: 1, devices: std::ptr::null() };
+        let mut ctx: *mut gs_multi = std::ptr::null_mut();
+        let st = unsafe { gs_multi_create(flat, &launch, &mut ctx) };
+        if st != GS_OK { return Err(std::io::Error::new(std::io::ErrorKind::Other, last_error())); }
+        Ok(Frames { ctx })
+    }
+    /// One frame's linear colour (W*H*3 f32) into `rgb`.
+    pub fn frame(&mut self, cam: &gs_camera, ss: &gs_sample_settings, seed: u64, rgb: &mut [f32]) -> std::io::Result<gs_stats> {
+        if rgb.len() < (cam.image_width as usize) * (cam.image_height as usize) * 3 {
+            return Err(std::io::Error::new(std::io::ErrorKind::InvalidInput, "rgb buffer too small"));
+        }
+        let outs = gs_multi_outputs { rgb: rgb.as_mut_ptr(), rgb8: std::ptr::null_mut(), ppm_text: std::ptr::null_mut(),
+                                      ppm_capacity: 0, ppm_len: std::ptr::null_mut() };
+        let mut stats = gs_stats::default();
+        let st = unsafe { gs_multi_render(self.ctx, cam, ss, seed, &outs, &mut stats) };
+        if st != GS_OK { return Err(std::io::Error::new(std::io::ErrorKind::Other, last_error())); }
+        Ok(stats)
+    }
+}
+
+impl Drop for Frames {
+    fn drop(&mut self) { unsafe { gs_multi_destroy(self.ctx); } }
 }
 
 /// `Camera::render` (camera.rs:100-121) on `num_gpus` GPUs of this node (0 = all): the

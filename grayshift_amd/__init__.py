@@ -13,7 +13,7 @@ import importlib
 _EXPORTS = {
     "HostScene": "renderer", "Renderer": "renderer", "camera": "renderer", "render": "renderer",
     "set_tuning": "renderer", "write_ppm": "renderer", "render_ppm": "renderer", "ppm_encode_async": "renderer",
-    "render_multi": "renderer",
+    "render_multi": "renderer", "MultiRenderer": "renderer",
     "SceneBuilder": "scene", "camera_spec": "scene", "fixed_spp": "scene", "sample_settings": "scene",
 }
 _SUBMODULES = {"scenes", "partition", "assets", "_native", "scene", "codeobj"}

@@ -16,7 +16,7 @@ GS_OBJ_LIST, GS_OBJ_BVH, GS_OBJ_TRANSLATE, GS_OBJ_ROTATE_Y, GS_OBJ_CUBE, GS_OBJ_
 GS_MAT_LAMBERTIAN, GS_MAT_METAL, GS_MAT_DIELECTRIC, GS_MAT_DIFFUSE_LIGHT, GS_MAT_ISOTROPIC = 1, 2, 3, 4, 5
 GS_TEX_SOLID, GS_TEX_CHECKERED, GS_TEX_IMAGE, GS_TEX_NOISE = 1, 2, 3, 4
 GS_BG_SOLID, GS_BG_HDRI = 1, 2
-GS_ABI_VERSION = 5
+GS_ABI_VERSION = 6
 GS_OK, GS_ERR_ARG, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPORTED, GS_ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5
 
 D3 = C.c_double * 3
@@ -137,7 +137,12 @@ class gs_stats(C.Structure):
     _fields_ = [("counters", gs_counters), ("setup_ms", C.c_double), ("total_ms", C.c_double),
                 ("render_ms_max", C.c_double), ("render_ms_min", C.c_double), ("gather_ms", C.c_double),
                 ("algorithmic_bytes", C.c_uint64), ("gathered_bytes", C.c_uint64), ("num_gpus", C.c_int32),
-                ("pad", C.c_int32)]
+                ("pad", C.c_int32), ("kernel_ms_max", C.c_double), ("kernel_ms_min", C.c_double)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("counters", "pad")}
+        d["counters"] = self.counters.as_dict()
+        return d
 
 
 class gs_scene_info(C.Structure):
@@ -173,7 +178,7 @@ SIGNATURES = {
     "gs_ppm_scratch_bytes": (C.c_int64, [C.c_int32, C.c_int32]),
     "gs_ppm_encode_async": (C.c_int32, [_P, C.c_int32, C.c_int32, _P, C.c_int64, _P, _P, C.c_int64, _P]),
     "gs_render_ppm": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64, _P,
-                                  C.c_int64, C.POINTER(C.c_int64), C.POINTER(gs_counters)]),
+                                  C.c_int64, C.POINTER(C.c_int64), C.POINTER(gs_stats)]),
     "gs_plan_tiles": (C.c_int32, [_P, C.POINTER(gs_camera), C.c_uint64, C.c_int32, C.c_int32, C.c_int32, _P,
                                   C.c_int64, C.POINTER(C.c_int32)]),
     "gs_unpack_tiles_part_async": (C.c_int32, [C.POINTER(gs_camera), C.POINTER(gs_partition), C.c_int64, _P, _P,
@@ -181,21 +186,30 @@ SIGNATURES = {
     "gs_device_alloc": (C.c_int32, [C.c_int64, C.POINTER(_P)]),
     "gs_device_free": (C.c_int32, [_P]),
     "gs_device_upload": (C.c_int32, [_P, _P, C.c_int64]),
+    "gs_device_download": (C.c_int32, [_P, _P, C.c_int64]),
     "gs_render": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64, _P,
-                              C.POINTER(gs_counters)]),
+                              C.POINTER(gs_stats)]),
     "gs_render_multi": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64,
                                     C.POINTER(gs_launch), C.POINTER(gs_multi_outputs), C.POINTER(gs_stats)]),
     "gs_rccl_library": (C.c_char_p, []),
+    "gs_multi_create": (C.c_int32, [_P, C.POINTER(gs_launch), C.POINTER(_P)]),
+    "gs_multi_render": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64,
+                                    C.POINTER(gs_multi_outputs), C.POINTER(gs_stats)]),
+    "gs_multi_frame": (C.c_int32, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(C.c_int32)]),
+    "gs_multi_devices": (C.c_int32, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int32]),
+    "gs_multi_scene": (C.c_int32, [_P, C.c_int32, C.POINTER(_P)]),
+    "gs_multi_destroy": (C.c_int32, [_P]),
+    "gs_debug_set_multi_collective": (C.c_int32, [C.c_int32]),
     # grayshift_host.h
     "gs_host_scene_from_spec": (C.c_int32, [C.POINTER(gs_scene_spec), C.POINTER(_P)]),
     "gs_host_scene_destroy": (C.c_int32, [_P]),
     "gs_host_scene_flat": (_P, [_P]),
     "gs_host_camera": (C.c_int32, [C.POINTER(gs_camera_spec), C.POINTER(gs_camera)]),
     "gs_host_render_spec": (C.c_int32, [C.POINTER(gs_scene_spec), C.POINTER(gs_camera_spec),
-                                        C.POINTER(gs_sample_settings), C.c_uint64, _P, C.POINTER(gs_counters)]),
+                                        C.POINTER(gs_sample_settings), C.c_uint64, _P, C.POINTER(gs_stats)]),
     "gs_host_render_ppm_spec": (C.c_int32, [C.POINTER(gs_scene_spec), C.POINTER(gs_camera_spec),
                                             C.POINTER(gs_sample_settings), C.c_uint64, _P, C.c_int64,
-                                            C.POINTER(C.c_int64), C.POINTER(gs_counters)]),
+                                            C.POINTER(C.c_int64), C.POINTER(gs_stats)]),
     "gs_host_write_ppm": (C.c_int32, [C.c_char_p, C.c_int32, C.c_int32, _P]),
     "gs_host_color_byte": (C.c_int32, [C.c_double]),
     "gs_host_noise_permutation": (None, [C.c_uint32, _P]),

@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "../../../include/grayshift_gpu.h"
+#include "../host/internal.hpp"
 #include "devmath.hpp"
 #include "geometry.hpp"
 #include "perlin.hpp"
@@ -1111,7 +1112,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         o[0] = LD(L_CSR);
         o[1] = LD(L_CSG);
         o[2] = LD(L_CSB);
-#ifndef GS_STAMPS
+#if !defined(GS_STAMPS) && !defined(GS_CERT_CHECK)  // (those builds use item_visits as their record buffer)
         if (P->item_visits) atomicAdd(&P->item_visits[item / P->cpp], c_nodes);
 #endif
         atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
@@ -1154,7 +1155,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         o8[2] = color_byte(cb);
                     }
                     atomicAdd(&s_cnt[C_PIX], 1ull);
-#ifndef GS_STAMPS
+#if !defined(GS_STAMPS) && !defined(GS_CERT_CHECK)
                     if (P->item_visits) P->item_visits[item] = c_nodes;
 #endif
                     atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
@@ -1208,6 +1209,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     uint64_t acc_node = 0, acc_leaf = 0;  // stamps build: wave clock in node / leaf passes
     uint64_t dist_ref = 0, dist_kind = 0;  // stamps build: distinct leaf refs / ref kinds per leaf pass
     uint64_t it_all = 0, it_node = 0, it_leaf = 0, ln_node = 0, ln_leaf = 0, it_shade = 0, ln_shade = 0;
+    // stamps build: node steps (lanes) from global memory; wave node steps with any active lane,
+    // with any lane reading its record from global memory; active lanes over those steps
+    uint64_t d_gvis = 0, d_wsteps = 0, d_wsteps_g = 0, d_wlanes = 0;
 #pragma unroll 1
     for (;;) {
         // ---------------------------------------------------------- refill
@@ -1376,6 +1380,17 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #define GS_NODE_STEPS 8
 #endif
                 auto node_step = [&]() __attribute__((always_inline)) {
+#ifdef GS_STAMPS
+                {
+                    const bool glob = !((FEAT & GS_FEAT_LDSTREE) != 0) && cur < THR_END && cur >= (A.lds_nodes << 5);
+                    const uint64_t act = __builtin_amdgcn_ballot_w64(cur < THR_END);
+                    const uint64_t gl = __builtin_amdgcn_ballot_w64(glob);
+                    d_gvis += glob;
+                    d_wsteps += act != 0;
+                    d_wsteps_g += gl != 0;
+                    d_wlanes += (uint64_t)__popcll(act);
+                }
+#endif
                 if (cur < THR_END) {
                     // One 32-B record (2 x 16 B off the SGPR base, offset = cur << 5), the
                     // box test, and the next record: the hit link or the miss link.
@@ -1638,6 +1653,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         atomicAdd(&dbg[17], (unsigned long long)dist_ref);
         atomicAdd(&dbg[18], (unsigned long long)dist_kind);
     }
+    if (P->item_visits && d_gvis) atomicAdd(&((unsigned long long*)P->item_visits)[19], (unsigned long long)d_gvis);
     if (lane == 0 && P->item_visits) {
         unsigned long long* dbg = (unsigned long long*)P->item_visits;
         atomicAdd(&dbg[0], (unsigned long long)acc_refill);
@@ -1653,6 +1669,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         for (int k = 0; k < 5; k++) atomicAdd(&dbg[10 + k], s_reg[(tid >> 6) * 8 + k]);
         atomicAdd(&dbg[15], (unsigned long long)acc_node);
         atomicAdd(&dbg[16], (unsigned long long)acc_leaf);
+        atomicAdd(&dbg[20], (unsigned long long)d_wsteps);
+        atomicAdd(&dbg[21], (unsigned long long)d_wsteps_g);
+        atomicAdd(&dbg[22], (unsigned long long)d_wlanes);
 
     }
 #endif
@@ -1771,6 +1790,7 @@ struct LaunchSlot {
     double* partial = nullptr;  // chunk partial sums, grown on demand
     size_t partial_bytes = 0;
     hipEvent_t done = nullptr;  // recorded after the slot's last launch
+    hipStream_t stream = nullptr;  // the stream of the slot's last launch
     bool used = false;
 };
 static const int kLaunchSlots = 4;
@@ -2479,6 +2499,17 @@ gs_status gs_render_tiles_debug_async(const gs_device_scene* ds, const gs_camera
 gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
                                    uint64_t seed, const gs_partition* part, const gs_render_outputs* outs,
                                    gs_counters* d_counters, void* stream) {
+    return gs_render_tiles_timed_async(ds, cam, ss, seed, part, outs, d_counters, stream, nullptr, nullptr);
+}
+
+}  // extern "C"
+
+// The launch behind gs_render_tiles_ex_async; k_begin / k_end (nullable, timing events of
+// the stream's device) are recorded right around the megakernel, so a caller can time the
+// dominant kernel alone (csrc/host/internal.hpp; the frame context's gs_stats.kernel_ms).
+gs_status gs_render_tiles_timed_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
+                                      uint64_t seed, const gs_partition* part, const gs_render_outputs* outs,
+                                      gs_counters* d_counters, void* stream, hipEvent_t k_begin, hipEvent_t k_end) {
     if (!ds || !cam || !ss || !part || !outs || (!outs->rgb && !outs->rgb8)) return fail(GS_ERR_ARG, "null argument");
     if (!part_ok(cam, part)) return fail(GS_ERR_ARG, "bad partition / image size");
     if (ss->batch_size == 0) return fail(GS_ERR_ARG, "batch_size 0 never terminates (camera.rs:137)");
@@ -2600,11 +2631,32 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     if ((uint64_t)kp.n_items + (uint64_t)kp.claim * (waves + 1) >= 0xFFFFFFFFull)
         return fail(GS_ERR_ARG, "too many work items for the 32-bit work queue");
 
-    // This launch's slot: wait (on `st`) for the slot's previous launch before reusing it.
-    LaunchSlot& sl = mds->slots[mds->next_slot++ % kLaunchSlots];
-    if (sl.used) HIPCHK(hipStreamWaitEvent(st, sl.done, 0));
+    // This launch's slot.  A slot whose last launch ran on this very stream is reused first:
+    // stream order already puts the new launch behind the old one, so one caller on one
+    // stream keeps one slot (and one chunk-sum buffer) however many launches it queues.
+    // Otherwise a slot whose launch has finished, preferring one whose chunk sums are big
+    // enough; otherwise the next in turn, behind a stream wait on its previous launch.
+    const size_t need_partial = chunk ? (size_t)kp.n_items * 3 * sizeof(double) : 0;
+    int pick = -1;
+    for (int k = 0; k < kLaunchSlots && pick < 0; k++)
+        if (mds->slots[k].used && mds->slots[k].stream == st) pick = k;
+    if (pick < 0) {
+        int idle = -1;
+        for (int k = 0; k < kLaunchSlots; k++) {
+            LaunchSlot& c = mds->slots[k];
+            if (c.used && hipEventQuery(c.done) != hipSuccess) continue;
+            if (c.partial_bytes >= need_partial) {
+                idle = k;
+                break;
+            }
+            if (idle < 0) idle = k;
+        }
+        pick = idle >= 0 ? idle : (int)(mds->next_slot++ % kLaunchSlots);
+    }
+    LaunchSlot& sl = mds->slots[pick];
+    if (sl.used && sl.stream != st) HIPCHK(hipStreamWaitEvent(st, sl.done, 0));
     if (chunk) {
-        const size_t need = (size_t)kp.n_items * 3 * sizeof(double);
+        const size_t need = need_partial;
         if (sl.partial_bytes < need) {
             if (sl.used) HIPCHK(hipEventSynchronize(sl.done));  // nothing in flight reads it
             if (sl.partial) (void)hipFree(sl.partial);
@@ -2622,8 +2674,10 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     hipLaunchKernelGGL(gs_params_kernel, dim3(1), dim3(64), 0, st, kp, sl.params);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(sl.queue, 0, 4, st));
+    if (k_begin) HIPCHK(hipEventRecord(k_begin, st));
     hipLaunchKernelGGL(kernel_for(lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
+    if (k_end) HIPCHK(hipEventRecord(k_end, st));
     if (chunk) {
         const unsigned grid = (unsigned)std::min<int64_t>((cap + 255) / 256, 8192);
         hipLaunchKernelGGL(gs_combine_kernel, dim3(grid), dim3(256), 0, st, (const KParams*)sl.params);
@@ -2631,52 +2685,11 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
     }
     HIPCHK(hipEventRecord(sl.done, st));
     sl.used = true;
+    sl.stream = st;
     return GS_OK;
 }
 
-gs_status gs_render(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
-                    float* out_rgb, gs_counters* counters) {
-    if (!scene || !cam || !ss || !out_rgb) return fail(GS_ERR_ARG, "null argument");
-    gs_device_scene* ds = nullptr;
-    gs_status r = gs_device_scene_create(scene, &ds);
-    if (r != GS_OK) return r;
-    gs_partition p{0, 1, 64, 64};
-    int64_t cap = gs_partition_capacity(cam, &p);
-    if (cap < 0) {
-        gs_device_scene_destroy(ds);
-        return fail(GS_ERR_ARG, "bad image size");
-    }
-    const size_t W = (size_t)cam->image_width, H = (size_t)cam->image_height;
-    float *d_pack = nullptr, *d_frame = nullptr;
-    gs_counters* d_cnt = nullptr;
-    auto cleanup = [&]() {
-        if (d_pack) (void)hipFree(d_pack);
-        if (d_frame) (void)hipFree(d_frame);
-        if (d_cnt) (void)hipFree(d_cnt);
-        gs_device_scene_destroy(ds);
-    };
-    if (hipMalloc(&d_pack, (size_t)cap * 12 + 16) != hipSuccess || hipMalloc(&d_frame, W * H * 12 + 16) != hipSuccess ||
-        hipMalloc(&d_cnt, sizeof(gs_counters)) != hipSuccess) {
-        cleanup();
-        return fail(GS_ERR_OOM, "hipMalloc failed");
-    }
-    hipError_t e = hipMemset(d_cnt, 0, sizeof(gs_counters));
-    if (e == hipSuccess) e = hipMemset(d_frame, 0, W * H * 12);
-    if (e != hipSuccess) {
-        cleanup();
-        return fail(GS_ERR_HIP, hipGetErrorString(e));
-    }
-    r = gs_render_tiles_async(ds, cam, ss, seed, &p, d_pack, d_cnt, nullptr);
-    if (r == GS_OK) r = gs_unpack_tiles_async(cam, 1, p.tile_w, p.tile_h, cap, d_pack, d_frame, nullptr);
-    if (r == GS_OK) {
-        e = hipDeviceSynchronize();
-        if (e == hipSuccess) e = hipMemcpy(out_rgb, d_frame, W * H * 12, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && counters) e = hipMemcpy(counters, d_cnt, sizeof(gs_counters), hipMemcpyDeviceToHost);
-        if (e != hipSuccess) r = fail(GS_ERR_HIP, hipGetErrorString(e));
-    }
-    cleanup();
-    return r;
-}
+extern "C" {
 
 gs_status gs_plan_tiles(const gs_device_scene* ds, const gs_camera* cam, uint64_t seed, int32_t world,
                         int32_t tile_w, int32_t tile_h, int32_t* order_out, int64_t order_cap,
@@ -2763,66 +2776,10 @@ gs_status gs_device_upload(void* d_dst, const void* src, int64_t bytes) {
     HIPCHK(hipMemcpy(d_dst, src, (size_t)bytes, hipMemcpyHostToDevice));
     return GS_OK;
 }
-
-gs_status gs_render_ppm(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
-                        char* out_text, int64_t text_capacity, int64_t* out_len, gs_counters* counters) {
-    if (!scene || !cam || !ss || !out_text || !out_len) return fail(GS_ERR_ARG, "null argument");
-    const int64_t need = gs_ppm_max_bytes(cam->image_width, cam->image_height);
-    if (need < 0) return fail(GS_ERR_ARG, "bad image size");
-    if (text_capacity < need) return fail(GS_ERR_ARG, "text capacity below gs_ppm_max_bytes");
-    gs_device_scene* ds = nullptr;
-    gs_status r = gs_device_scene_create(scene, &ds);
-    if (r != GS_OK) return r;
-    gs_partition p{0, 1, 64, 64};
-    const int64_t cap = gs_partition_capacity(cam, &p);
-    const size_t W = (size_t)cam->image_width, H = (size_t)cam->image_height;
-    const int64_t scratch = gs_ppm_scratch_bytes(cam->image_width, cam->image_height);
-    uint8_t *d_pack = nullptr, *d_frame = nullptr;
-    char* d_text = nullptr;
-    void* d_scratch = nullptr;
-    int64_t* d_len = nullptr;
-    gs_counters* d_cnt = nullptr;
-    auto cleanup = [&]() {
-        if (d_pack) (void)hipFree(d_pack);
-        if (d_frame) (void)hipFree(d_frame);
-        if (d_text) (void)hipFree(d_text);
-        if (d_scratch) (void)hipFree(d_scratch);
-        if (d_len) (void)hipFree(d_len);
-        if (d_cnt) (void)hipFree(d_cnt);
-        gs_device_scene_destroy(ds);
-    };
-    if (hipMalloc(&d_pack, (size_t)cap * 3 + 16) != hipSuccess || hipMalloc(&d_frame, W * H * 3 + 16) != hipSuccess ||
-        hipMalloc(&d_text, (size_t)need) != hipSuccess || hipMalloc(&d_scratch, (size_t)scratch) != hipSuccess ||
-        hipMalloc(&d_len, 8) != hipSuccess || hipMalloc(&d_cnt, sizeof(gs_counters)) != hipSuccess) {
-        cleanup();
-        return fail(GS_ERR_OOM, "hipMalloc failed");
-    }
-    hipError_t e = hipMemset(d_cnt, 0, sizeof(gs_counters));
-    if (e != hipSuccess) {
-        cleanup();
-        return fail(GS_ERR_HIP, hipGetErrorString(e));
-    }
-    gs_render_outputs o{nullptr, d_pack, nullptr};
-    r = gs_render_tiles_ex_async(ds, cam, ss, seed, &p, &o, d_cnt, nullptr);
-    if (r == GS_OK) r = gs_unpack_tiles_u8_async(cam, 1, p.tile_w, p.tile_h, cap, d_pack, d_frame, nullptr);
-    if (r == GS_OK)
-        r = gs_ppm_encode_async(d_frame, cam->image_width, cam->image_height, d_text, need, d_len, d_scratch, scratch,
-                                nullptr);
-    if (r == GS_OK) {
-        int64_t len = 0;
-        e = hipDeviceSynchronize();
-        if (e == hipSuccess) e = hipMemcpy(&len, d_len, 8, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && (len <= 0 || len > need)) {
-            cleanup();
-            return fail(GS_ERR_HIP, "PPM encoder returned a bad length");
-        }
-        if (e == hipSuccess) e = hipMemcpy(out_text, d_text, (size_t)len, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && counters) e = hipMemcpy(counters, d_cnt, sizeof(gs_counters), hipMemcpyDeviceToHost);
-        if (e != hipSuccess) r = fail(GS_ERR_HIP, hipGetErrorString(e));
-        else *out_len = len;
-    }
-    cleanup();
-    return r;
+gs_status gs_device_download(void* dst, const void* d_src, int64_t bytes) {
+    if (!dst || !d_src || bytes < 0) return fail(GS_ERR_ARG, "bad argument");
+    HIPCHK(hipMemcpy(dst, d_src, (size_t)bytes, hipMemcpyDeviceToHost));
+    return GS_OK;
 }
 
 }  // extern "C"

@@ -51,18 +51,18 @@ static void check(gs_status st) {
     if (st != GS_OK) throw std::runtime_error(std::string("gs_render failed: ") + gs_last_error());
 }
 
-void Camera::render_linear(const Hittable& world, float* out_rgb, gs_counters* counters, uint64_t seed) const {
+void Camera::render_linear(const Hittable& world, float* out_rgb, gs_stats* stats, uint64_t seed) const {
     auto fs = flatten_world(world, bg);
-    check(gs_render(&fs->view, &cam, &ss, seed, out_rgb, counters));
+    check(gs_render(&fs->view, &cam, &ss, seed, out_rgb, stats));
 }
 
-std::string Camera::render_ppm(const Hittable& world, gs_counters* counters, uint64_t seed) const {
+std::string Camera::render_ppm(const Hittable& world, gs_stats* stats, uint64_t seed) const {
     auto fs = flatten_world(world, bg);
     const int64_t cap = gs_ppm_max_bytes(cam.image_width, cam.image_height);
     if (cap < 0) throw std::runtime_error("bad image size");
     std::string text((size_t)cap, '\0');
     int64_t len = 0;
-    check(gs_render_ppm(&fs->view, &cam, &ss, seed, &text[0], cap, &len, counters));
+    check(gs_render_ppm(&fs->view, &cam, &ss, seed, &text[0], cap, &len, stats));
     text.resize((size_t)len);
     return text;
 }

@@ -194,7 +194,7 @@ gs_status gs_host_camera(const gs_camera_spec* c, gs_camera* out) {
 }
 
 gs_status gs_host_render_spec(const gs_scene_spec* spec, const gs_camera_spec* c, const gs_sample_settings* ss,
-                              uint64_t seed, float* out_rgb, gs_counters* counters) {
+                              uint64_t seed, float* out_rgb, gs_stats* stats) {
     if (!spec || !c || !ss || !out_rgb) return fail(GS_ERR_ARG, "null argument");
     return guarded([&]() {
         SpecBuilder b(*spec);
@@ -204,13 +204,13 @@ gs_status gs_host_render_spec(const gs_scene_spec* spec, const gs_camera_spec* c
                    Vec3(c->look_at[0], c->look_at[1], c->look_at[2]), Vec3(c->vup[0], c->vup[1], c->vup[2]),
                    c->defocus_angle, c->focus_distance, b.background());
         auto fs = flatten_world(*world, cam.background());
-        return gs_render(&fs->view, &cam.fields(), &cam.settings(), seed, out_rgb, counters);
+        return gs_render(&fs->view, &cam.fields(), &cam.settings(), seed, out_rgb, stats);
     });
 }
 
 gs_status gs_host_render_ppm_spec(const gs_scene_spec* spec, const gs_camera_spec* c, const gs_sample_settings* ss,
                                   uint64_t seed, char* out_text, int64_t text_capacity, int64_t* out_len,
-                                  gs_counters* counters) {
+                                  gs_stats* stats) {
     if (!spec || !c || !ss || !out_text || !out_len) return fail(GS_ERR_ARG, "null argument");
     return guarded([&]() {
         SpecBuilder b(*spec);
@@ -221,7 +221,7 @@ gs_status gs_host_render_ppm_spec(const gs_scene_spec* spec, const gs_camera_spe
                    c->defocus_angle, c->focus_distance, b.background());
         auto fs = flatten_world(*world, cam.background());
         return gs_render_ppm(&fs->view, &cam.fields(), &cam.settings(), seed, out_text, text_capacity, out_len,
-                             counters);
+                             stats);
     });
 }
 

@@ -1,0 +1,15 @@
+// internal.hpp — library-internal entry points shared by render.hip and the host files
+// (not part of the C-ABI in include/).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include "../../../include/grayshift_gpu.h"
+
+extern "C" void gs_set_last_error(const char* msg);
+
+// gs_render_tiles_ex_async with two optional timing events (of the stream's device)
+// recorded right before and after the megakernel itself, so the frame context can report
+// the dominant kernel's time apart from the parameter, queue and chunk-combine launches.
+gs_status gs_render_tiles_timed_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
+                                      uint64_t seed, const gs_partition* part, const gs_render_outputs* outs,
+                                      gs_counters* d_counters, void* stream, hipEvent_t k_begin, hipEvent_t k_end);

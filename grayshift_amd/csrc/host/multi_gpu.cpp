@@ -1,13 +1,16 @@
-// multi_gpu.cpp — the N-GPU render behind one C-ABI call (gs_render_multi).
+// multi_gpu.cpp — the frame context behind the synchronous C-ABI calls: gs_multi_* (one
+// world on N GPUs, many frames), and gs_render_multi / gs_render / gs_render_ppm on top.
 //
 // Replaces the reference's whole pixel loop, camera.rs:105-114 (pixel list, rayon
 // `par_iter` over every pixel, `collect_into_vec`), across the GPUs of one node from a
-// single host thread: the scene is uploaded to every device, the frame is cut into
-// tiles (cost-balanced plan from a 1-spp pilot on the first device, or round-robin),
-// every device renders its tiles into a packed buffer on its own stream, one grouped
-// RCCL gather over xGMI brings the packed buffers to the first device, which unpacks
-// them into the frame (and, optionally, formats the PPM text, camera.rs:101-103,116-118).
-// Pixels carry their own RNG streams, so the frame is the same for any device count.
+// single host thread: at creation the scene is uploaded to every device and one RCCL
+// communicator is built (ncclCommInitAll, N > 1); per frame the image is cut into tiles
+// (cost-balanced plan from a 1-spp pilot on the first device, kept while the camera is
+// unchanged, or round-robin), every device renders its tiles into a packed buffer on its
+// own stream, one grouped RCCL gather over xGMI brings the packed buffers to the first
+// device, which unpacks them into the frame (and, optionally, formats the PPM text,
+// camera.rs:101-103,116-118).  Pixels carry their own RNG streams, so the frame is the
+// same for any device count.
 //
 // RCCL is resolved at run time (dlopen), so single-GPU users never load it, and the copy
 // that matches the process's HIP runtime is used (torch bundles both: one HIP runtime
@@ -23,8 +26,7 @@
 #include <vector>
 
 #include "../../../include/grayshift_gpu.h"
-
-extern "C" void gs_set_last_error(const char* msg);
+#include "internal.hpp"
 
 namespace {
 
@@ -36,6 +38,7 @@ gs_status fail(gs_status code, const std::string& msg) {
 struct Rccl {
     decltype(&ncclCommInitAll) comm_init_all = nullptr;
     decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclCommAbort) comm_abort = nullptr;
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGather) gather = nullptr;
@@ -75,12 +78,14 @@ const Rccl& rccl() {
         }
         r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
         r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+        r.comm_abort = (decltype(r.comm_abort))dlsym(h, "ncclCommAbort");
         r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
         r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
         r.gather = (decltype(r.gather))dlsym(h, "ncclGather");
         r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
-        r.ok = r.comm_init_all && r.comm_destroy && r.group_start && r.group_end && r.gather && r.error_string;
-        if (!r.ok) r.error = r.path + " lacks ncclCommInitAll/ncclGather";
+        r.ok = r.comm_init_all && r.comm_destroy && r.comm_abort && r.group_start && r.group_end && r.gather &&
+               r.error_string;
+        if (!r.ok) r.error = r.path + " lacks ncclCommInitAll/ncclCommAbort/ncclGather";
     });
     return r;
 }
@@ -98,54 +103,33 @@ void add_counters(gs_counters& a, const gs_counters& b) {
     for (size_t k = 0; k < sizeof(gs_counters) / sizeof(uint64_t); k++) pa[k] += pb[k];
 }
 
-// Everything one call allocates, released on every exit path.
+// A device buffer grown on demand (contents not kept).
+struct DBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    bool ensure(size_t need) {
+        if (bytes >= need && p) return true;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (hipMalloc(&p, need + 16) != hipSuccess) return false;
+        bytes = need;
+        return true;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
 struct Device {
     int id = 0;
     gs_device_scene* scene = nullptr;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // render start/end, gather start/end
-    int32_t* d_order = nullptr;
-    float* d_packed = nullptr;
-    uint8_t* d_packed8 = nullptr;
-    gs_counters* d_cnt = nullptr;
-};
-
-struct Job {
-    std::vector<Device> dev;
-    std::vector<ncclComm_t> comms;
-    float *d_gathered = nullptr, *d_frame = nullptr;
-    uint8_t *d_gathered8 = nullptr, *d_frame8 = nullptr;
-    char* d_text = nullptr;
-    void* d_scratch = nullptr;
-    int64_t* d_len = nullptr;
-    int saved = 0;
-    ~Job() {
-        for (auto& d : dev) {
-            (void)hipSetDevice(d.id);
-            if (d.stream) (void)hipStreamSynchronize(d.stream);
-        }
-        if (!comms.empty() && rccl().ok)
-            for (auto c : comms)
-                if (c) rccl().comm_destroy(c);
-        for (auto& d : dev) {
-            (void)hipSetDevice(d.id);
-            for (auto e : d.ev)
-                if (e) (void)hipEventDestroy(e);
-            if (d.d_order) (void)hipFree(d.d_order);
-            if (d.d_packed) (void)hipFree(d.d_packed);
-            if (d.d_packed8) (void)hipFree(d.d_packed8);
-            if (d.d_cnt) (void)hipFree(d.d_cnt);
-            if (d.scene) gs_device_scene_destroy(d.scene);
-            if (d.stream) (void)hipStreamDestroy(d.stream);
-        }
-        if (!dev.empty()) {
-            (void)hipSetDevice(dev[0].id);
-            for (void* p : {(void*)d_gathered, (void*)d_frame, (void*)d_gathered8, (void*)d_frame8, (void*)d_text,
-                            d_scratch, (void*)d_len})
-                if (p) (void)hipFree(p);
-        }
-        (void)hipSetDevice(saved);
-    }
+    // render start / end, megakernel start / end, gather + unpack start / end
+    hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    DBuf order, packed, packed8, cnt;
 };
 
 #define HIPOK(x)                                                                                     \
@@ -153,13 +137,263 @@ struct Job {
         hipError_t e_ = (x);                                                                         \
         if (e_ != hipSuccess) return fail(GS_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
-#define ALLOC(p, n)                                                                                           \
-    do {                                                                                                      \
-        if (hipMalloc((void**)&(p), (size_t)(n) + 16) != hipSuccess)                                         \
-            return fail(GS_ERR_OOM, "hipMalloc of " + std::to_string((long long)(n)) + " bytes failed");      \
+#define GROW(buf, n)                                                                                            \
+    do {                                                                                                        \
+        if (!(buf).ensure((size_t)(n)))                                                                         \
+            return fail(GS_ERR_OOM, "hipMalloc of " + std::to_string((long long)(n)) + " bytes failed");       \
     } while (0)
 
+// Restores the caller's current device on every exit path.
+struct DeviceGuard {
+    int saved = 0;
+    DeviceGuard() { (void)hipGetDevice(&saved); }
+    ~DeviceGuard() { (void)hipSetDevice(saved); }
+};
+
+int g_collective_always = 0;  // gs_debug_set_multi_collective
+
 }  // namespace
+
+struct gs_multi {
+    std::vector<Device> dev;
+    std::vector<int> ids;
+    std::vector<ncclComm_t> comms;  // one rank per device (N > 1, or forced by the test hook)
+    bool comms_broken = false;      // a collective failed: the communicators were aborted
+    int32_t tw = 64, th = 64;
+    bool plan = false;
+    std::mutex mu;
+    // tile partition of the last camera (plan or round-robin)
+    bool part_ready = false;
+    gs_camera part_cam{};
+    std::vector<int32_t> order;  // empty: round-robin
+    int32_t slots = 0;
+    int64_t cap = 0;  // packed pixels per rank
+    // the first device's gather and frame buffers
+    DBuf gathered, gathered8, frame, frame8, text, scratch, len;
+    bool have_rgb = false, have_rgb8 = false;
+    int32_t frame_w = 0, frame_h = 0;
+
+    ~gs_multi() {
+        DeviceGuard g;
+        if (!comms_broken)
+            for (auto& d : dev) {
+                (void)hipSetDevice(d.id);
+                if (d.stream) (void)hipStreamSynchronize(d.stream);
+            }
+        if (!comms.empty() && rccl().ok)
+            for (auto c : comms)
+                if (c) (comms_broken ? rccl().comm_abort(c) : rccl().comm_destroy(c));
+        for (auto& d : dev) {
+            (void)hipSetDevice(d.id);
+            for (auto e : d.ev)
+                if (e) (void)hipEventDestroy(e);
+            d.order.release();
+            d.packed.release();
+            d.packed8.release();
+            d.cnt.release();
+            if (d.scene) gs_device_scene_destroy(d.scene);
+            if (d.stream) (void)hipStreamDestroy(d.stream);
+        }
+        if (!dev.empty()) {
+            (void)hipSetDevice(dev[0].id);
+            for (DBuf* b : {&gathered, &gathered8, &frame, &frame8, &text, &scratch, &len}) b->release();
+        }
+    }
+
+    // Abort the communicators after a failed collective: its peers may never join, so the
+    // streams holding it must not be waited on (destroy skips the stream syncs).
+    gs_status collective_failed(const std::string& what) {
+        if (rccl().ok)
+            for (auto& c : comms)
+                if (c) rccl().comm_abort(c);
+        comms.clear();
+        comms_broken = true;
+        return fail(GS_ERR_HIP, what);
+    }
+
+    gs_status partition(const gs_camera* cam, uint64_t seed, double* plan_ms);
+    gs_status render(const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed, const gs_multi_outputs* out,
+                     gs_stats* stats);
+};
+
+gs_status gs_multi::partition(const gs_camera* cam, uint64_t seed, double* plan_ms) {
+    if (part_ready && std::memcmp(&part_cam, cam, sizeof(gs_camera)) == 0) return GS_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int n = (int)dev.size();
+    part_ready = false;
+    order.clear();
+    slots = 0;
+    if (plan && n > 1) {
+        HIPOK(hipSetDevice(dev[0].id));
+        gs_status s = gs_plan_tiles(dev[0].scene, cam, seed, n, tw, th, nullptr, 0, &slots);
+        if (s != GS_OK) return s;
+        order.resize((size_t)slots * n);
+        s = gs_plan_tiles(dev[0].scene, cam, seed, n, tw, th, order.data(), (int64_t)order.size(), &slots);
+        if (s != GS_OK) return s;
+        for (auto& d : dev) {
+            HIPOK(hipSetDevice(d.id));
+            GROW(d.order, order.size() * sizeof(int32_t));
+            HIPOK(hipMemcpy(d.order.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        }
+        cap = (int64_t)slots * tw * th;
+    } else {
+        gs_partition p0{0, n, tw, th, nullptr, 0, 0};
+        cap = gs_partition_capacity(cam, &p0);  // rank 0 holds the most tiles
+        if (cap < 0) return fail(GS_ERR_ARG, "bad partition");
+    }
+    part_cam = *cam;
+    part_ready = true;
+    *plan_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return GS_OK;
+}
+
+gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
+                           const gs_multi_outputs* out, gs_stats* stats) {
+    if (!cam || !ss) return fail(GS_ERR_ARG, "null argument");
+    if (out && !out->rgb && !out->rgb8 && !out->ppm_text) return fail(GS_ERR_ARG, "no output requested");
+    if (out && out->ppm_text && !out->ppm_len) return fail(GS_ERR_ARG, "ppm_text without ppm_len");
+    if (cam->image_width <= 0 || cam->image_height <= 0) return fail(GS_ERR_ARG, "bad image size");
+    if (out && out->ppm_text && out->ppm_capacity < gs_ppm_max_bytes(cam->image_width, cam->image_height))
+        return fail(GS_ERR_ARG, "ppm_capacity below gs_ppm_max_bytes");
+    if (comms_broken) return fail(GS_ERR_HIP, "the context's communicator was aborted after a failed collective");
+    std::lock_guard<std::mutex> lock(mu);
+    DeviceGuard guard;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int n = (int)dev.size();
+    double plan_ms = 0.0;
+    gs_status s = partition(cam, seed, &plan_ms);
+    if (s != GS_OK) return s;
+    const bool want_rgb = !out || out->rgb;
+    const bool want8 = out && (out->rgb8 || out->ppm_text);
+    const int64_t W = cam->image_width, H = cam->image_height;
+    have_rgb = have_rgb8 = false;
+
+    // Render: every device its own tiles, concurrently (launches are asynchronous).
+    for (int i = 0; i < n; i++) {
+        Device& d = dev[i];
+        HIPOK(hipSetDevice(d.id));
+        if (want_rgb) GROW(d.packed, cap * 12);
+        if (want8) GROW(d.packed8, cap * 3);
+        GROW(d.cnt, sizeof(gs_counters));
+        HIPOK(hipMemsetAsync(d.cnt.p, 0, sizeof(gs_counters), d.stream));
+        gs_partition p{i, n, tw, th, order.empty() ? nullptr : (const int32_t*)d.order.p, slots, 0};
+        gs_render_outputs o{want_rgb ? (float*)d.packed.p : nullptr, want8 ? (uint8_t*)d.packed8.p : nullptr,
+                            nullptr};
+        HIPOK(hipEventRecord(d.ev[0], d.stream));
+        s = gs_render_tiles_timed_async(d.scene, cam, ss, seed, &p, &o, (gs_counters*)d.cnt.p, d.stream, d.ev[2],
+                                        d.ev[3]);
+        if (s != GS_OK) return s;
+        HIPOK(hipEventRecord(d.ev[1], d.stream));
+    }
+    Device& d0 = dev[0];
+    HIPOK(hipSetDevice(d0.id));
+    if (want_rgb) GROW(frame, W * H * 12);
+    if (want8) GROW(frame8, W * H * 3);
+    const void* src = want_rgb ? d0.packed.p : nullptr;
+    const void* src8 = want8 ? d0.packed8.p : nullptr;
+    if (!comms.empty()) {
+        // One grouped RCCL gather of the packed tiles to the first device (rank-major, as
+        // gs_unpack_tiles_part_async reads them).
+        if (want_rgb) GROW(gathered, (int64_t)n * cap * 12);
+        if (want8) GROW(gathered8, (int64_t)n * cap * 3);
+        const Rccl& R = rccl();
+        for (int i = 0; i < n; i++) {
+            HIPOK(hipSetDevice(dev[i].id));
+            HIPOK(hipEventRecord(dev[i].ev[4], dev[i].stream));
+        }
+        if (R.group_start() != ncclSuccess) return collective_failed("ncclGroupStart failed");
+        ncclResult_t rc = ncclSuccess;
+        for (int i = 0; i < n && rc == ncclSuccess; i++) {
+            Device& d = dev[i];
+            (void)hipSetDevice(d.id);
+            if (want_rgb)
+                rc = R.gather(d.packed.p, i == 0 ? gathered.p : nullptr, (size_t)cap * 3, ncclFloat32, 0, comms[i],
+                              d.stream);
+            if (rc == ncclSuccess && want8)
+                rc = R.gather(d.packed8.p, i == 0 ? gathered8.p : nullptr, (size_t)cap * 3, ncclUint8, 0, comms[i],
+                              d.stream);
+        }
+        const ncclResult_t rc2 = R.group_end();
+        if (rc != ncclSuccess || rc2 != ncclSuccess)
+            return collective_failed(std::string("ncclGather: ") + R.error_string(rc != ncclSuccess ? rc : rc2));
+        HIPOK(hipSetDevice(d0.id));
+        src = gathered.p;
+        src8 = gathered8.p;
+    } else {
+        HIPOK(hipEventRecord(d0.ev[4], d0.stream));
+    }
+    gs_partition pu{0, n, tw, th, order.empty() ? nullptr : (const int32_t*)d0.order.p, slots, 0};
+    if (want_rgb) {
+        s = gs_unpack_tiles_part_async(cam, &pu, cap, src, frame.p, 12, d0.stream);
+        if (s != GS_OK) return s;
+    }
+    if (want8) {
+        s = gs_unpack_tiles_part_async(cam, &pu, cap, src8, frame8.p, 3, d0.stream);
+        if (s != GS_OK) return s;
+    }
+    if (out && out->ppm_text) {
+        const int64_t need = gs_ppm_max_bytes(cam->image_width, cam->image_height);
+        const int64_t sb = gs_ppm_scratch_bytes(cam->image_width, cam->image_height);
+        GROW(text, need);
+        GROW(scratch, sb);
+        GROW(len, 8);
+        s = gs_ppm_encode_async((const uint8_t*)frame8.p, cam->image_width, cam->image_height, (char*)text.p, need,
+                                (int64_t*)len.p, scratch.p, sb, d0.stream);
+        if (s != GS_OK) return s;
+    }
+    HIPOK(hipEventRecord(d0.ev[5], d0.stream));
+    // Wait, then results.
+    gs_counters total{};
+    double rmax = 0.0, rmin = 1e300, kmax = 0.0, kmin = 1e300;
+    for (int i = 0; i < n; i++) {
+        Device& d = dev[i];
+        HIPOK(hipSetDevice(d.id));
+        HIPOK(hipStreamSynchronize(d.stream));
+        gs_counters c{};
+        HIPOK(hipMemcpy(&c, d.cnt.p, sizeof(c), hipMemcpyDeviceToHost));
+        add_counters(total, c);
+        float ms = 0.0f, kms = 0.0f;
+        HIPOK(hipEventElapsedTime(&ms, d.ev[0], d.ev[1]));
+        HIPOK(hipEventElapsedTime(&kms, d.ev[2], d.ev[3]));
+        rmax = std::max(rmax, (double)ms);
+        rmin = std::min(rmin, (double)ms);
+        kmax = std::max(kmax, (double)kms);
+        kmin = std::min(kmin, (double)kms);
+    }
+    HIPOK(hipSetDevice(d0.id));
+    float gms = 0.0f;
+    HIPOK(hipEventElapsedTime(&gms, d0.ev[4], d0.ev[5]));
+    have_rgb = want_rgb;
+    have_rgb8 = want8;
+    frame_w = cam->image_width;
+    frame_h = cam->image_height;
+    if (out && out->rgb) HIPOK(hipMemcpy(out->rgb, frame.p, (size_t)(W * H * 12), hipMemcpyDeviceToHost));
+    if (out && out->rgb8) HIPOK(hipMemcpy(out->rgb8, frame8.p, (size_t)(W * H * 3), hipMemcpyDeviceToHost));
+    if (out && out->ppm_text) {
+        int64_t l = 0;
+        HIPOK(hipMemcpy(&l, len.p, 8, hipMemcpyDeviceToHost));
+        if (l <= 0 || l > out->ppm_capacity) return fail(GS_ERR_HIP, "PPM encoder returned a bad length");
+        HIPOK(hipMemcpy(out->ppm_text, text.p, (size_t)l, hipMemcpyDeviceToHost));
+        *out->ppm_len = l;
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        stats->counters = total;
+        stats->setup_ms = plan_ms;
+        stats->total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        stats->render_ms_max = rmax;
+        stats->render_ms_min = rmin;
+        stats->kernel_ms_max = kmax;
+        stats->kernel_ms_min = kmin;
+        stats->gather_ms = gms;
+        stats->algorithmic_bytes = algorithmic_bytes(total);
+        stats->gathered_bytes =
+            comms.empty() ? 0 : (uint64_t)n * (uint64_t)cap * ((want_rgb ? 12u : 0u) + (want8 ? 3u : 0u));
+        stats->num_gpus = n;
+    }
+    return GS_OK;
+}
 
 extern "C" {
 
@@ -168,16 +402,16 @@ const char* gs_rccl_library(void) {
     return r.ok ? r.path.c_str() : nullptr;
 }
 
-gs_status gs_render_multi(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
-                          const gs_launch* launch, const gs_multi_outputs* out, gs_stats* stats) {
-    if (!scene || !cam || !ss || !launch || !out) return fail(GS_ERR_ARG, "null argument");
-    if (!out->rgb && !out->rgb8 && !out->ppm_text) return fail(GS_ERR_ARG, "no output requested");
-    if (out->ppm_text && !out->ppm_len) return fail(GS_ERR_ARG, "ppm_text without ppm_len");
-    if (cam->image_width <= 0 || cam->image_height <= 0) return fail(GS_ERR_ARG, "bad image size");
+gs_status gs_multi_create(const gs_flat_scene* scene, const gs_launch* launch, gs_multi** out) {
+    if (!scene || !launch || !out) return fail(GS_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (launch->num_gpus <= 0 && launch->devices)
+        return fail(GS_ERR_ARG, "num_gpus <= 0 (every visible device) with a device list");
     int visible = 0;
     if (hipGetDeviceCount(&visible) != hipSuccess || visible == 0) return fail(GS_ERR_NO_DEVICE, "no HIP device visible");
     const int n = launch->num_gpus > 0 ? launch->num_gpus : visible;
-    if (n > visible) return fail(GS_ERR_ARG, "num_gpus " + std::to_string(n) + " > visible devices " + std::to_string(visible));
+    if (n > visible)
+        return fail(GS_ERR_ARG, "num_gpus " + std::to_string(n) + " > visible devices " + std::to_string(visible));
     std::vector<int> ids(n);
     for (int i = 0; i < n; i++) {
         ids[i] = launch->devices ? launch->devices[i] : i;
@@ -185,171 +419,124 @@ gs_status gs_render_multi(const gs_flat_scene* scene, const gs_camera* cam, cons
         for (int j = 0; j < i; j++)
             if (ids[j] == ids[i]) return fail(GS_ERR_ARG, "device listed twice (one communicator rank per device)");
     }
-    const int32_t tw = launch->tile_w > 0 ? launch->tile_w : 64, th = launch->tile_h > 0 ? launch->tile_h : tw;
-    const int64_t W = cam->image_width, H = cam->image_height;
-    const bool want8 = out->rgb8 || out->ppm_text;
-    if (out->ppm_text && out->ppm_capacity < gs_ppm_max_bytes(cam->image_width, cam->image_height))
-        return fail(GS_ERR_ARG, "ppm_capacity below gs_ppm_max_bytes");
-    const Rccl& R = rccl();
-    if (!R.ok) return fail(GS_ERR_UNSUPPORTED, "RCCL unavailable: " + R.error);
-
-    const auto t0 = std::chrono::steady_clock::now();
-    Job job;
-    (void)hipGetDevice(&job.saved);
-    job.dev.resize(n);
+    if (launch->tile_w < 0 || launch->tile_h < 0) return fail(GS_ERR_ARG, "negative tile size");
+    const bool collective = n > 1 || g_collective_always;
+    if (collective && !rccl().ok) return fail(GS_ERR_UNSUPPORTED, "RCCL unavailable: " + rccl().error);
+    DeviceGuard guard;
+    auto m = new gs_multi();
+    m->ids = ids;
+    m->tw = launch->tile_w > 0 ? launch->tile_w : 64;
+    m->th = launch->tile_h > 0 ? launch->tile_h : m->tw;
+    m->plan = launch->plan != 0;
+    m->dev.resize(n);
+    auto bail = [&](gs_status st) {
+        delete m;
+        return st;
+    };
     for (int i = 0; i < n; i++) {
-        Device& d = job.dev[i];
+        Device& d = m->dev[i];
         d.id = ids[i];
-        HIPOK(hipSetDevice(d.id));
+        if (hipSetDevice(d.id) != hipSuccess) return bail(fail(GS_ERR_HIP, "hipSetDevice failed"));
         const gs_status s = gs_device_scene_create(scene, &d.scene);
-        if (s != GS_OK) return s;
-        HIPOK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-        for (auto& e : d.ev) HIPOK(hipEventCreate(&e));
+        if (s != GS_OK) return bail(s);
+        if (hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess)
+            return bail(fail(GS_ERR_HIP, "hipStreamCreateWithFlags failed"));
+        for (auto& e : d.ev)
+            if (hipEventCreate(&e) != hipSuccess) return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
     }
-    // Partition: every rank gets the same packed capacity (rank 0 holds the most tiles).
-    std::vector<int32_t> order;
-    int32_t slots = 0;
-    if (launch->plan && n > 1) {
-        HIPOK(hipSetDevice(job.dev[0].id));
-        gs_status s = gs_plan_tiles(job.dev[0].scene, cam, seed, n, tw, th, nullptr, 0, &slots);
-        if (s != GS_OK) return s;
-        order.resize((size_t)slots * n);
-        s = gs_plan_tiles(job.dev[0].scene, cam, seed, n, tw, th, order.data(), (int64_t)order.size(), &slots);
-        if (s != GS_OK) return s;
-    }
-    gs_partition p0{0, n, tw, th, nullptr, 0, 0};
-    const int64_t cap = order.empty() ? gs_partition_capacity(cam, &p0) : (int64_t)slots * tw * th;
-    if (cap < 0) return fail(GS_ERR_ARG, "bad partition");
-    const auto t1 = std::chrono::steady_clock::now();
-
-    for (int i = 0; i < n; i++) {
-        Device& d = job.dev[i];
-        HIPOK(hipSetDevice(d.id));
-        if (!order.empty()) {
-            ALLOC(d.d_order, order.size() * sizeof(int32_t));
-            HIPOK(hipMemcpyAsync(d.d_order, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                                 d.stream));
-        }
-        if (out->rgb) ALLOC(d.d_packed, cap * 12);
-        if (want8) ALLOC(d.d_packed8, cap * 3);
-        ALLOC(d.d_cnt, sizeof(gs_counters));
-        if (d.d_packed) HIPOK(hipMemsetAsync(d.d_packed, 0, (size_t)cap * 12, d.stream));
-        if (d.d_packed8) HIPOK(hipMemsetAsync(d.d_packed8, 0, (size_t)cap * 3, d.stream));
-        HIPOK(hipMemsetAsync(d.d_cnt, 0, sizeof(gs_counters), d.stream));
-        if (i == 0) {
-            if (out->rgb) {
-                ALLOC(job.d_gathered, (int64_t)n * cap * 12);
-                ALLOC(job.d_frame, W * H * 12);
-            }
-            if (want8) {
-                ALLOC(job.d_gathered8, (int64_t)n * cap * 3);
-                ALLOC(job.d_frame8, W * H * 3);
-            }
-            if (out->ppm_text) {
-                ALLOC(job.d_text, gs_ppm_max_bytes(cam->image_width, cam->image_height));
-                ALLOC(job.d_scratch, gs_ppm_scratch_bytes(cam->image_width, cam->image_height));
-                ALLOC(job.d_len, 8);
-            }
-        }
-    }
-    // One communicator rank per device, rank i = device i of the list.
-    job.comms.assign(n, nullptr);
-    {
-        ncclResult_t rc = R.comm_init_all(job.comms.data(), n, ids.data());
+    if (collective) {  // one communicator rank per device, rank i = device i of the list
+        m->comms.assign(n, nullptr);
+        const ncclResult_t rc = rccl().comm_init_all(m->comms.data(), n, ids.data());
         if (rc != ncclSuccess) {
-            job.comms.clear();
-            return fail(GS_ERR_HIP, std::string("ncclCommInitAll: ") + R.error_string(rc));
+            m->comms.clear();
+            return bail(fail(GS_ERR_HIP, std::string("ncclCommInitAll: ") + rccl().error_string(rc)));
         }
     }
-    // Render: every device its own tiles, concurrently.
-    for (int i = 0; i < n; i++) {
-        Device& d = job.dev[i];
-        HIPOK(hipSetDevice(d.id));
-        gs_partition p{i, n, tw, th, d.d_order, slots, 0};
-        gs_render_outputs o{d.d_packed, d.d_packed8, nullptr};
-        HIPOK(hipEventRecord(d.ev[0], d.stream));
-        const gs_status s = gs_render_tiles_ex_async(d.scene, cam, ss, seed, &p, &o, d.d_cnt, d.stream);
-        if (s != GS_OK) return s;
-        HIPOK(hipEventRecord(d.ev[1], d.stream));
-    }
-    // One grouped RCCL gather of the packed tiles to the first device (rank-major, as
-    // gs_unpack_tiles_part_async reads them).
-    if (R.group_start() != ncclSuccess) return fail(GS_ERR_HIP, "ncclGroupStart failed");
-    ncclResult_t rc = ncclSuccess;
-    for (int i = 0; i < n && rc == ncclSuccess; i++) {
-        Device& d = job.dev[i];
-        (void)hipSetDevice(d.id);
-        (void)hipEventRecord(d.ev[2], d.stream);
-        if (d.d_packed)
-            rc = R.gather(d.d_packed, i == 0 ? (void*)job.d_gathered : nullptr, (size_t)cap * 3, ncclFloat32, 0,
-                          job.comms[i], d.stream);
-        if (rc == ncclSuccess && d.d_packed8)
-            rc = R.gather(d.d_packed8, i == 0 ? (void*)job.d_gathered8 : nullptr, (size_t)cap * 3, ncclUint8, 0,
-                          job.comms[i], d.stream);
-    }
-    const ncclResult_t rc2 = R.group_end();
-    if (rc != ncclSuccess || rc2 != ncclSuccess)
-        return fail(GS_ERR_HIP, std::string("ncclGather: ") + R.error_string(rc != ncclSuccess ? rc : rc2));
-    Device& d0 = job.dev[0];
-    HIPOK(hipSetDevice(d0.id));
-    gs_partition pu{0, n, tw, th, d0.d_order, slots, 0};
-    if (out->rgb) {
-        const gs_status s = gs_unpack_tiles_part_async(cam, &pu, cap, job.d_gathered, job.d_frame, 12, d0.stream);
-        if (s != GS_OK) return s;
-    }
-    if (want8) {
-        const gs_status s = gs_unpack_tiles_part_async(cam, &pu, cap, job.d_gathered8, job.d_frame8, 3, d0.stream);
-        if (s != GS_OK) return s;
-    }
-    HIPOK(hipEventRecord(d0.ev[3], d0.stream));
-    if (out->ppm_text) {
-        const int64_t need = gs_ppm_max_bytes(cam->image_width, cam->image_height);
-        const gs_status s = gs_ppm_encode_async(job.d_frame8, cam->image_width, cam->image_height, job.d_text, need,
-                                                job.d_len, job.d_scratch,
-                                                gs_ppm_scratch_bytes(cam->image_width, cam->image_height), d0.stream);
-        if (s != GS_OK) return s;
-    }
-    // Results to the host.
-    gs_counters total{};
-    double rmax = 0.0, rmin = 1e300;
-    for (int i = 0; i < n; i++) {
-        Device& d = job.dev[i];
-        HIPOK(hipSetDevice(d.id));
-        HIPOK(hipStreamSynchronize(d.stream));
-        gs_counters c{};
-        HIPOK(hipMemcpy(&c, d.d_cnt, sizeof(c), hipMemcpyDeviceToHost));
-        add_counters(total, c);
-        float ms = 0.0f;
-        HIPOK(hipEventElapsedTime(&ms, d.ev[0], d.ev[1]));
-        rmax = std::max(rmax, (double)ms);
-        rmin = std::min(rmin, (double)ms);
-    }
-    HIPOK(hipSetDevice(d0.id));
-    float gms = 0.0f;
-    HIPOK(hipEventElapsedTime(&gms, d0.ev[2], d0.ev[3]));
-    if (out->rgb) HIPOK(hipMemcpy(out->rgb, job.d_frame, (size_t)(W * H * 12), hipMemcpyDeviceToHost));
-    if (out->rgb8) HIPOK(hipMemcpy(out->rgb8, job.d_frame8, (size_t)(W * H * 3), hipMemcpyDeviceToHost));
-    if (out->ppm_text) {
-        int64_t len = 0;
-        HIPOK(hipMemcpy(&len, job.d_len, 8, hipMemcpyDeviceToHost));
-        if (len <= 0 || len > out->ppm_capacity) return fail(GS_ERR_HIP, "PPM encoder returned a bad length");
-        HIPOK(hipMemcpy(out->ppm_text, job.d_text, (size_t)len, hipMemcpyDeviceToHost));
-        *out->ppm_len = len;
-    }
-    const auto t2 = std::chrono::steady_clock::now();
-    if (stats) {
-        std::memset(stats, 0, sizeof(*stats));
-        stats->counters = total;
-        stats->setup_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-        stats->total_ms = std::chrono::duration<double, std::milli>(t2 - t0).count();
-        stats->render_ms_max = rmax;
-        stats->render_ms_min = rmin;
-        stats->gather_ms = gms;
-        stats->algorithmic_bytes = algorithmic_bytes(total);
-        stats->gathered_bytes = (uint64_t)n * (uint64_t)cap * ((out->rgb ? 12u : 0u) + (want8 ? 3u : 0u));
-        stats->num_gpus = n;
-    }
+    *out = m;
     return GS_OK;
+}
+
+gs_status gs_multi_render(gs_multi* m, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
+                          const gs_multi_outputs* out, gs_stats* stats) {
+    if (!m) return fail(GS_ERR_ARG, "null context");
+    return m->render(cam, ss, seed, out, stats);
+}
+
+gs_status gs_multi_frame(const gs_multi* m, const float** d_rgb, const uint8_t** d_rgb8, int32_t* device) {
+    if (!m) return fail(GS_ERR_ARG, "null context");
+    if (d_rgb) *d_rgb = m->have_rgb ? (const float*)m->frame.p : nullptr;
+    if (d_rgb8) *d_rgb8 = m->have_rgb8 ? (const uint8_t*)m->frame8.p : nullptr;
+    if (device) *device = m->dev[0].id;
+    return GS_OK;
+}
+
+gs_status gs_multi_devices(const gs_multi* m, int32_t* num_gpus, int32_t* devices, int32_t capacity) {
+    if (!m || !num_gpus) return fail(GS_ERR_ARG, "null argument");
+    *num_gpus = (int32_t)m->ids.size();
+    if (devices)
+        for (int32_t i = 0; i < *num_gpus && i < capacity; i++) devices[i] = m->ids[i];
+    return GS_OK;
+}
+
+gs_status gs_multi_scene(const gs_multi* m, int32_t rank, const gs_device_scene** scene) {
+    if (!m || !scene) return fail(GS_ERR_ARG, "null argument");
+    if (rank < 0 || rank >= (int32_t)m->dev.size()) return fail(GS_ERR_ARG, "rank out of range");
+    *scene = m->dev[rank].scene;
+    return GS_OK;
+}
+
+gs_status gs_debug_set_multi_collective(int32_t always) {
+    g_collective_always = always ? 1 : 0;
+    return GS_OK;
+}
+
+gs_status gs_multi_destroy(gs_multi* m) {
+    delete m;
+    return GS_OK;
+}
+
+gs_status gs_render_multi(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
+                          const gs_launch* launch, const gs_multi_outputs* out, gs_stats* stats) {
+    if (!scene || !cam || !ss || !launch || !out) return fail(GS_ERR_ARG, "null argument");
+    const auto t0 = std::chrono::steady_clock::now();
+    gs_multi* m = nullptr;
+    gs_status s = gs_multi_create(scene, launch, &m);
+    if (s != GS_OK) return s;
+    const auto t1 = std::chrono::steady_clock::now();
+    s = m->render(cam, ss, seed, out, stats);
+    gs_multi_destroy(m);
+    if (s == GS_OK && stats) {
+        stats->setup_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return s;
+}
+
+// The one-device, one-frame calls: a context on the current device, no collective.
+static gs_status render_here(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss,
+                             uint64_t seed, const gs_multi_outputs* out, gs_stats* stats) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail(GS_ERR_NO_DEVICE, "no HIP device visible");
+    const int32_t ids[1] = {dev};
+    gs_launch l{1, 64, 64, 0, ids};
+    return gs_render_multi(scene, cam, ss, seed, &l, out, stats);
+}
+
+gs_status gs_render(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
+                    float* out_rgb, gs_stats* stats) {
+    if (!scene || !cam || !ss || !out_rgb) return fail(GS_ERR_ARG, "null argument");
+    gs_multi_outputs o{out_rgb, nullptr, nullptr, 0, nullptr};
+    return render_here(scene, cam, ss, seed, &o, stats);
+}
+
+gs_status gs_render_ppm(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
+                        char* out_text, int64_t text_capacity, int64_t* out_len, gs_stats* stats) {
+    if (!scene || !cam || !ss || !out_text || !out_len) return fail(GS_ERR_ARG, "null argument");
+    const int64_t need = gs_ppm_max_bytes(cam->image_width, cam->image_height);
+    if (need < 0) return fail(GS_ERR_ARG, "bad image size");
+    if (text_capacity < need) return fail(GS_ERR_ARG, "text capacity below gs_ppm_max_bytes");
+    gs_multi_outputs o{nullptr, nullptr, out_text, text_capacity, out_len};
+    return render_here(scene, cam, ss, seed, &o, stats);
 }
 
 }  // extern "C"

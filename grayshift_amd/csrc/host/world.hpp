@@ -360,9 +360,9 @@ public:
     // camera.rs:100 — same contract: PPM "P3" text, one `r g b` line per pixel.
     void render(const Hittable& world, std::ostream& image_file, uint64_t seed = 1) const;
     // The linear framebuffer (pixel_color / sample_count, camera.rs:167) instead of PPM.
-    void render_linear(const Hittable& world, float* out_rgb, gs_counters* counters, uint64_t seed = 1) const;
+    void render_linear(const Hittable& world, float* out_rgb, gs_stats* stats, uint64_t seed = 1) const;
     // The PPM text Camera::render writes (device-formatted).
-    std::string render_ppm(const Hittable& world, gs_counters* counters, uint64_t seed = 1) const;
+    std::string render_ppm(const Hittable& world, gs_stats* stats, uint64_t seed = 1) const;
     const gs_camera& fields() const { return cam; }
     const gs_sample_settings& settings() const { return ss; }
     const Background& background() const { return bg; }

@@ -19,14 +19,17 @@ def camera(cam_spec):
     return out
 
 
-def render(scene, seed=1):
-    """Render a scenes.Scene on the current HIP device.  Returns (rgb [H,W,3] f32, counters)."""
+def render(scene, seed=1, stats=None):
+    """Render a scenes.Scene on the current HIP device.  Returns (rgb [H,W,3] f32, counters);
+    `stats` (a dict, optional) receives the call's gs_stats (kernel / render ms, bytes)."""
     cam = camera(scene.camera)
     out = np.zeros((cam.image_height, cam.image_width, 3), dtype=np.float32)
-    cnt = N.gs_counters()
+    st = N.gs_stats()
     N.check(N.lib.gs_host_render_spec(scene.spec.ptr(), C.byref(scene.camera), C.byref(scene.settings), seed,
-                                      out.ctypes.data, C.byref(cnt)))
-    return out, cnt.as_dict()
+                                      out.ctypes.data, C.byref(st)))
+    if stats is not None:
+        stats.update(st.as_dict())
+    return out, st.counters.as_dict()
 
 
 def render_ppm(scene, seed=1):
@@ -38,10 +41,42 @@ def render_ppm(scene, seed=1):
         raise ValueError("bad image size")
     buf = C.create_string_buffer(int(cap))
     n = C.c_int64()
-    cnt = N.gs_counters()
+    st = N.gs_stats()
     N.check(N.lib.gs_host_render_ppm_spec(scene.spec.ptr(), C.byref(scene.camera), C.byref(scene.settings), seed,
-                                          buf, cap, C.byref(n), C.byref(cnt)))
-    return buf.raw[:n.value], cnt.as_dict()
+                                          buf, cap, C.byref(n), C.byref(st)))
+    return buf.raw[:n.value], st.counters.as_dict()
+
+
+def _launch(num_gpus, tile, plan, devices):
+    dev = None
+    if devices is not None:
+        dev = (C.c_int32 * len(devices))(*devices)
+        num_gpus = len(devices)
+    launch = N.gs_launch(num_gpus=num_gpus, tile_w=tile, tile_h=tile, plan=1 if plan else 0,
+                         devices=C.cast(dev, C.c_void_p) if dev is not None else None)
+    return launch, dev
+
+
+def _outputs(W, H, rgb, rgb8, ppm):
+    """gs_multi_outputs for the requested host outputs (None: the frame stays on the device)."""
+    if not (rgb or rgb8 or ppm):
+        return None, {}, None
+    res = {}
+    out = N.gs_multi_outputs()
+    if rgb:
+        res["rgb"] = np.zeros((H, W, 3), dtype=np.float32)
+        out.rgb = res["rgb"].ctypes.data
+    if rgb8:
+        res["rgb8"] = np.zeros((H, W, 3), dtype=np.uint8)
+        out.rgb8 = res["rgb8"].ctypes.data
+    ppm_buf = None
+    if ppm:
+        cap = N.lib.gs_ppm_max_bytes(W, H)
+        ppm_buf = (C.create_string_buffer(int(cap)), C.c_int64(0))
+        out.ppm_text = C.addressof(ppm_buf[0])
+        out.ppm_capacity = cap
+        out.ppm_len = C.pointer(ppm_buf[1])
+    return out, res, ppm_buf
 
 
 def render_multi(scene, num_gpus=0, seed=1, tile=64, plan=True, rgb=True, rgb8=False, ppm=False, devices=None):
@@ -53,38 +88,89 @@ def render_multi(scene, num_gpus=0, seed=1, tile=64, plan=True, rgb=True, rgb8=F
     host = HostScene(scene.spec)
     try:
         cam = camera(scene.camera)
-        H, W = cam.image_height, cam.image_width
-        res = {}
-        out = N.gs_multi_outputs()
-        if rgb:
-            res["rgb"] = np.zeros((H, W, 3), dtype=np.float32)
-            out.rgb = res["rgb"].ctypes.data
-        if rgb8:
-            res["rgb8"] = np.zeros((H, W, 3), dtype=np.uint8)
-            out.rgb8 = res["rgb8"].ctypes.data
-        n = C.c_int64(0)
-        if ppm:
-            cap = N.lib.gs_ppm_max_bytes(W, H)
-            buf = C.create_string_buffer(int(cap))
-            out.ppm_text = C.addressof(buf)
-            out.ppm_capacity = cap
-            out.ppm_len = C.pointer(n)
-        dev = None
-        if devices is not None:
-            dev = (C.c_int32 * len(devices))(*devices)
-            num_gpus = len(devices)
-        launch = N.gs_launch(num_gpus=num_gpus, tile_w=tile, tile_h=tile, plan=1 if plan else 0,
-                             devices=C.cast(dev, C.c_void_p) if dev is not None else None)
+        out, res, ppm_buf = _outputs(cam.image_width, cam.image_height, rgb, rgb8, ppm)
+        if out is None:
+            out = N.gs_multi_outputs()  # none requested: the library reports GS_ERR_ARG
+        launch, _dev = _launch(num_gpus, tile, plan, devices)
         st = N.gs_stats()
         N.check(N.lib.gs_render_multi(host.flat_ptr, C.byref(cam), C.byref(scene.settings), seed, C.byref(launch),
                                       C.byref(out), C.byref(st)))
         if ppm:
-            res["ppm"] = buf.raw[:n.value]
-        res["counters"] = {k: int(getattr(st.counters, k)) for k in N.COUNTER_NAMES}
-        res["stats"] = {k: getattr(st, k) for k, _ in N.gs_stats._fields_ if k not in ("counters", "pad")}
+            res["ppm"] = ppm_buf[0].raw[:ppm_buf[1].value]
+        res["counters"] = st.counters.as_dict()
+        res["stats"] = {k: v for k, v in st.as_dict().items() if k != "counters"}
         return res
     finally:
         host.close()
+
+
+class MultiRenderer:
+    """The persistent N-GPU frame context (gs_multi_*): the world uploaded to every device
+    and the RCCL communicator built once, then any number of frames, each one synchronous
+    call (plan, render on every device, one gather, unpack).  num_gpus=0: every visible
+    device; num_gpus=1: no collective."""
+
+    def __init__(self, scene, num_gpus=1, tile=64, plan=True, devices=None):
+        self.scene = scene
+        self.host = HostScene(scene.spec)
+        self.cam = camera(scene.camera)
+        self.settings = scene.settings
+        launch, _dev = _launch(num_gpus, tile, plan, devices)
+        h = C.c_void_p()
+        N.check(N.lib.gs_multi_create(self.host.flat_ptr, C.byref(launch), C.byref(h)))
+        self.handle = h
+        n = C.c_int32()
+        ids = (C.c_int32 * 64)()
+        N.check(N.lib.gs_multi_devices(h, C.byref(n), ids, 64))
+        self.devices = list(ids[:n.value])
+
+    @property
+    def width(self):
+        return self.cam.image_width
+
+    @property
+    def height(self):
+        return self.cam.image_height
+
+    def render(self, seed=1, rgb=False, rgb8=False, ppm=False):
+        """One frame.  With no host output requested the linear f32 frame stays on the first
+        device (frame_ptr()).  Returns a dict: requested outputs, "counters", "stats"."""
+        out, res, ppm_buf = _outputs(self.width, self.height, rgb, rgb8, ppm)
+        st = N.gs_stats()
+        N.check(N.lib.gs_multi_render(self.handle, C.byref(self.cam), C.byref(self.settings), seed,
+                                      C.byref(out) if out is not None else None, C.byref(st)))
+        if ppm:
+            res["ppm"] = ppm_buf[0].raw[:ppm_buf[1].value]
+        res["counters"] = st.counters.as_dict()
+        res["stats"] = {k: v for k, v in st.as_dict().items() if k != "counters"}
+        return res
+
+    def scene_info(self, rank=0):
+        """gs_device_scene_info of the scene on rank `rank`'s device."""
+        d = C.c_void_p()
+        N.check(N.lib.gs_multi_scene(self.handle, rank, C.byref(d)))
+        i = N.gs_scene_info()
+        N.check(N.lib.gs_device_scene_info(d, C.byref(i)))
+        return {k: getattr(i, k) for k, _ in N.gs_scene_info._fields_}
+
+    def frame_ptr(self):
+        """(device pointer of the last W*H*3 f32 frame or None, its device id)."""
+        p, p8, d = C.c_void_p(), C.c_void_p(), C.c_int32()
+        N.check(N.lib.gs_multi_frame(self.handle, C.byref(p), C.byref(p8), C.byref(d)))
+        return p.value, d.value
+
+    def close(self):
+        if getattr(self, "handle", None):
+            N.lib.gs_multi_destroy(self.handle)
+            self.handle = None
+        if getattr(self, "host", None):
+            self.host.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001  (interpreter shutdown: the binding may be gone)
+            pass
 
 
 def ppm_encode_async(d_rgb8, width, height, d_text, text_capacity, d_len, d_scratch, scratch_bytes, stream=0):

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 5
+#define GS_ABI_VERSION 6
 
 typedef int32_t gs_status;
 enum {
@@ -256,6 +256,26 @@ typedef struct gs_scene_info {
 } gs_scene_info;
 gs_status gs_device_scene_info(const gs_device_scene* scene, gs_scene_info* out);
 
+/* What one frame did (SURVEY.md §5 metrics row): filled by gs_render, gs_render_ppm,
+ * gs_render_multi and gs_multi_render (ABI 6; before ABI 6 only gs_render_multi, and
+ * gs_render / gs_render_ppm took a gs_counters*).  Times are HIP events on the launch
+ * streams (device) or the host clock (host). */
+typedef struct gs_stats {
+    gs_counters counters;       /* work done, summed over devices (exact, = the oracle's) */
+    double setup_ms;            /* host: scene uploads, communicator and tile plan of this call (one-shot
+                                   calls); gs_multi_render: the tile plan when it was (re)computed, else 0 */
+    double total_ms;            /* host: the whole call */
+    double render_ms_max;       /* slowest device's render: parameter + megakernel + chunk-combine launches */
+    double render_ms_min;       /* fastest device's */
+    double gather_ms;           /* first device: RCCL gather (N > 1) + unpack (+ PPM text when asked) */
+    uint64_t algorithmic_bytes; /* SURVEY.md §8d bytes of every launch (cache-served, not HBM) */
+    uint64_t gathered_bytes;    /* bytes the gather delivered to the first device (0 for one device) */
+    int32_t num_gpus;
+    int32_t pad;
+    double kernel_ms_max;       /* (ABI 6) the megakernel alone, slowest device */
+    double kernel_ms_min;       /* (ABI 6) the megakernel alone, fastest device */
+} gs_stats;
+
 /* Number of packed pixels (tiles * tile_w * tile_h) this rank renders. */
 int64_t gs_partition_capacity(const gs_camera* cam, const gs_partition* part);
 
@@ -322,7 +342,7 @@ gs_status gs_ppm_encode_async(const uint8_t* d_rgb8, int32_t width, int32_t heig
  * text_capacity >= gs_ppm_max_bytes(W, H) bytes; *out_len receives the length. */
 gs_status gs_render_ppm(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss,
                         uint64_t seed, char* out_text, int64_t text_capacity, int64_t* out_len,
-                        gs_counters* counters);
+                        gs_stats* stats /* nullable (ABI 6: was gs_counters*) */);
 
 /* Cost-balanced partition (ABI 3): a 1-spp pilot render of the whole frame on this
  * device (per-pixel BVH node visits, deterministic, so every rank computes the same
@@ -349,7 +369,7 @@ gs_status gs_unpack_tiles_part_async(const gs_camera* cam, const gs_partition* p
  * The frame equals gs_render's for every device count (per-pixel RNG streams).
  * Synchronous; RCCL is loaded at the first call (GS_ERR_UNSUPPORTED without it). */
 typedef struct gs_launch {
-    int32_t num_gpus;       /* devices used; 0 = every visible device */
+    int32_t num_gpus;       /* devices used; 0 = every visible device (devices must then be NULL) */
     int32_t tile_w, tile_h; /* 0 = 64 (tile_h 0 = tile_w) */
     int32_t plan;           /* 1: cost-balanced tiles, 0: round-robin */
     const int32_t* devices; /* nullable: num_gpus distinct HIP device ids (default 0..num_gpus-1) */
@@ -364,22 +384,35 @@ typedef struct gs_multi_outputs {
     int64_t* ppm_len;     /* receives the text length when ppm_text is set */
 } gs_multi_outputs;
 
-/* What one gs_render_multi call did (SURVEY.md §5 metrics). */
-typedef struct gs_stats {
-    gs_counters counters;       /* summed over devices */
-    double setup_ms;            /* host: scene uploads + tile plan */
-    double total_ms;            /* host: the whole call */
-    double render_ms_max;       /* slowest device's render launch (HIP events) */
-    double render_ms_min;       /* fastest device's */
-    double gather_ms;           /* first device: RCCL gather + unpack (HIP events) */
-    uint64_t algorithmic_bytes; /* SURVEY.md §8d bytes of every launch (cache-served, not HBM) */
-    uint64_t gathered_bytes;    /* bytes the gather delivered to the first device */
-    int32_t num_gpus;
-    int32_t pad;
-} gs_stats;
-
 gs_status gs_render_multi(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss,
                           uint64_t seed, const gs_launch* launch, const gs_multi_outputs* out, gs_stats* stats);
+
+/* ---- Persistent N-GPU frame context (ABI 6) ----
+ * gs_render_multi is gs_multi_create + one gs_multi_render + gs_multi_destroy.  A caller
+ * rendering many frames of one world (an animation, a benchmark) creates the context once:
+ * the scene upload to every device, the per-device streams and events and the RCCL
+ * communicator (ncclCommInitAll, N > 1 only) happen there, outside every frame.  The tile
+ * plan is computed at the first frame of a camera and kept while the camera is unchanged.
+ * launch->num_gpus <= 0 means every visible device and then requires devices == NULL.
+ * num_gpus == 1 uses no collective: the device unpacks its own tiles.
+ * A context is not reentrant: one gs_multi_render at a time (calls are serialised). */
+typedef struct gs_multi gs_multi;
+gs_status gs_multi_create(const gs_flat_scene* scene, const gs_launch* launch, gs_multi** out);
+/* One synchronous frame.  out: host outputs (any subset, at least one), or NULL: the linear
+ * f32 frame then stays on the first device (gs_multi_frame), nothing crosses PCIe. */
+gs_status gs_multi_render(gs_multi* m, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
+                          const gs_multi_outputs* out, gs_stats* stats);
+/* The last frame's device buffers on the first device (W*H*3 f32 / u8; NULL if that output
+ * was not produced), valid until the next gs_multi_render or gs_multi_destroy. */
+gs_status gs_multi_frame(const gs_multi* m, const float** d_rgb, const uint8_t** d_rgb8, int32_t* device);
+/* Devices of the context in rank order (devices: num_gpus entries, nullable). */
+gs_status gs_multi_devices(const gs_multi* m, int32_t* num_gpus, int32_t* devices, int32_t capacity);
+/* The device-resident scene of rank `rank` (e.g. for gs_device_scene_info); owned by the context. */
+gs_status gs_multi_scene(const gs_multi* m, int32_t rank, const gs_device_scene** scene);
+gs_status gs_multi_destroy(gs_multi* m);
+/* Test hook: 1 = contexts created from now on use the RCCL communicator and gather even for
+ * one device (so a one-GPU machine runs that code); 0 (default) = no collective for one. */
+gs_status gs_debug_set_multi_collective(int32_t always);
 
 /* Path of the RCCL library gs_render_multi uses (loaded on this call), or NULL. */
 const char* gs_rccl_library(void);
@@ -388,12 +421,14 @@ const char* gs_rccl_library(void);
 gs_status gs_device_alloc(int64_t bytes, void** d_out);
 gs_status gs_device_free(void* d_ptr);
 gs_status gs_device_upload(void* d_dst, const void* host_src, int64_t bytes);
+gs_status gs_device_download(void* host_dst, const void* d_src, int64_t bytes); /* (ABI 6) synchronous */
 
 /* Synchronous full-frame render on the current device: upload, render, copy back.
- * out_rgb: host buffer W*H*3 f32 (linear).  counters: host, nullable.  This is the
- * one-call replacement for camera.rs:105-114. */
+ * out_rgb: host buffer W*H*3 f32 (linear).  stats: host, nullable (counters, kernel and
+ * render times, algorithmic bytes).  This is the one-call replacement for camera.rs:105-114:
+ * gs_multi_create + gs_multi_render + gs_multi_destroy on the current device. */
 gs_status gs_render(const gs_flat_scene* scene, const gs_camera* cam, const gs_sample_settings* ss,
-                    uint64_t seed, float* out_rgb, gs_counters* counters);
+                    uint64_t seed, float* out_rgb, gs_stats* stats /* nullable (ABI 6: was gs_counters*) */);
 
 #ifdef __cplusplus
 }

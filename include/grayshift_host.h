@@ -30,15 +30,15 @@ const gs_flat_scene* gs_host_scene_flat(const gs_host_scene* scene);
 gs_status gs_host_camera(const gs_camera_spec* spec, gs_camera* out);
 
 /* Camera::render minus the PPM stage: spec -> world -> BVH -> flat -> gs_render.
- * out_rgb: host W*H*3 f32 linear.  counters: host, nullable. */
+ * out_rgb: host W*H*3 f32 linear.  stats: host, nullable (ABI 6: was gs_counters*). */
 gs_status gs_host_render_spec(const gs_scene_spec* spec, const gs_camera_spec* cam, const gs_sample_settings* ss,
-                              uint64_t seed, float* out_rgb, gs_counters* counters);
+                              uint64_t seed, float* out_rgb, gs_stats* stats);
 
 /* The whole of Camera::render (camera.rs:100-121): spec -> world -> BVH -> flat ->
  * gs_render_ppm.  out_text: host, >= gs_ppm_max_bytes(W, H); *out_len = text length. */
 gs_status gs_host_render_ppm_spec(const gs_scene_spec* spec, const gs_camera_spec* cam, const gs_sample_settings* ss,
                                   uint64_t seed, char* out_text, int64_t text_capacity, int64_t* out_len,
-                                  gs_counters* counters);
+                                  gs_stats* stats);
 
 /* Camera::render output stage on the host, from an f32 frame (camera.rs:101-103,116-118; color.rs:8-18). */
 gs_status gs_host_write_ppm(const char* path, int32_t width, int32_t height, const float* rgb);

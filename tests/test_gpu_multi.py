@@ -1,12 +1,15 @@
-"""gs_render_multi — the N-GPU render behind one C-ABI call (one process, one scene per
-device, one grouped RCCL gather over xGMI to the first device, unpack there) — and
-bench.py's torch.distributed gather over an RCCL process group.
+"""The frame context gs_multi_* (one process, one scene per device uploaded once, one
+grouped RCCL gather over xGMI to the first device per frame, unpack there), the one-shot
+gs_render_multi / gs_render / gs_render_ppm built on it, and bench.py's two launch modes
+(the context in one process; torch.distributed's gather over an RCCL process group).
 
 The box has one MI355X, so these run the RCCL code with a 1-rank communicator
-(ncclCommInitAll over one device / a 1-rank nccl process group): the frame must equal
-the single-GPU gs_render frame bit for bit, and the PPM text gs_render_ppm's byte for
-byte.  Multi-device partitions themselves are covered by test_gpu_parity.py
-(partition invariance, G in {1,2,3,4,8} on one GPU) and test_gpu_multiprocess.py."""
+(gs_debug_set_multi_collective forces ncclCommInitAll + ncclGather for one device; a
+1-rank nccl process group for bench.py): the frame must equal the single-GPU gs_render
+frame bit for bit, and the PPM text gs_render_ppm's byte for byte.  Multi-device
+partitions themselves are covered by test_gpu_parity.py (partition invariance and planned
+partitions, G in {1,2,3,4,8} on one GPU: the context's non-RCCL steps) and
+test_gpu_multiprocess.py.  The context's N > 1 path has not run on more than one device."""
 import json
 import os
 import socket
@@ -24,18 +27,113 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+class _collective:
+    """Force the RCCL communicator and gather for one-device contexts (test hook)."""
+    def __enter__(self):
+        N.check(N.lib.gs_debug_set_multi_collective(1))
+
+    def __exit__(self, *a):
+        N.check(N.lib.gs_debug_set_multi_collective(0))
+
+
 @pytest.mark.parametrize("plan", [False, True])
 @pytest.mark.parametrize("tile", [64, 24])
-def test_render_multi_one_gpu_equals_render(plan, tile):
+@pytest.mark.parametrize("rccl", [False, True])
+def test_render_multi_one_gpu_equals_render(plan, tile, rccl):
     sc = scenes.config("C4", width=160, spp=8)
     ref, rc = g.render(sc, seed=5)
-    res = g.render_multi(sc, num_gpus=1, seed=5, tile=tile, plan=plan, rgb=True, rgb8=True)
+    if rccl:
+        with _collective():
+            res = g.render_multi(sc, num_gpus=1, seed=5, tile=tile, plan=plan, rgb=True, rgb8=True)
+    else:
+        res = g.render_multi(sc, num_gpus=1, seed=5, tile=tile, plan=plan, rgb=True, rgb8=True)
     assert np.array_equal(res["rgb"], ref)
     assert res["counters"] == rc
     st = res["stats"]
     assert st["num_gpus"] == 1 and st["render_ms_max"] > 0 and st["gather_ms"] > 0
-    assert st["algorithmic_bytes"] > 0 and st["gathered_bytes"] > 0
-    assert N.lib.gs_rccl_library()  # RCCL was loaded and used
+    assert 0 < st["kernel_ms_max"] <= st["render_ms_max"]
+    assert st["algorithmic_bytes"] > 0
+    assert (st["gathered_bytes"] > 0) == rccl  # one device: no gather unless forced
+    if rccl:
+        assert N.lib.gs_rccl_library()  # RCCL was loaded and used
+
+
+def test_render_stats_on_the_single_gpu_calls():
+    """gs_render / gs_render_ppm fill gs_stats: counters equal the CPU
+    oracle's, kernel and render times from HIP events, algorithmic bytes (camera.rs:100-121)."""
+    import ctypes as C
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    sc = scenes.config("C4", width=96, spp=8)
+    host = g.HostScene(sc.spec)
+    cam = g.camera(sc.camera)
+    rgb = np.zeros((cam.image_height, cam.image_width, 3), np.float32)
+    st = N.gs_stats()
+    N.check(N.lib.gs_render(host.flat_ptr, C.byref(cam), C.byref(sc.settings), 4, rgb.ctypes.data, C.byref(st)))
+    ref, oc = oracle.render(sc, seed=4)
+    assert float(np.abs(rgb.astype(np.float64) - ref).max()) < 1e-3
+    assert st.counters.as_dict() == oc
+    assert st.num_gpus == 1 and 0 < st.kernel_ms_max <= st.render_ms_max and st.total_ms > 0
+    assert st.algorithmic_bytes > 0 and st.gathered_bytes == 0
+    cap = N.lib.gs_ppm_max_bytes(cam.image_width, cam.image_height)
+    buf = C.create_string_buffer(int(cap))
+    n = C.c_int64()
+    st2 = N.gs_stats()
+    N.check(N.lib.gs_render_ppm(host.flat_ptr, C.byref(cam), C.byref(sc.settings), 4, buf, cap, C.byref(n),
+                                C.byref(st2)))
+    assert st2.counters.as_dict() == oc and st2.kernel_ms_max > 0
+    host.close()
+
+
+@pytest.mark.parametrize("rccl", [False, True])
+def test_frame_context_many_frames(rccl):
+    """gs_multi_*: the scene is uploaded once; every frame of the context equals the
+    one-shot render of its seed, the device-resident frame equals the host copy, and the
+    stats report the megakernel alone inside the render."""
+    import ctypes as C
+    sc = scenes.config("C5", width=96, spp=4)
+    if rccl:
+        with _collective():
+            m = g.MultiRenderer(sc, num_gpus=1, tile=32, plan=True)
+    else:
+        m = g.MultiRenderer(sc, num_gpus=1, tile=32, plan=True)
+    assert m.devices == [0]
+    for seed in (1, 2, 1):
+        ref, rc = g.render(sc, seed=seed)
+        res = m.render(seed=seed, rgb=True)
+        assert np.array_equal(res["rgb"], ref) and res["counters"] == rc
+        dev = m.render(seed=seed)  # no host output: the frame stays on the device
+        p, d = m.frame_ptr()
+        assert p and d == 0 and dev["counters"] == rc
+        host = np.zeros_like(ref)
+        N.check(N.lib.gs_device_download(host.ctypes.data, C.c_void_p(p), host.nbytes))
+        assert np.array_equal(host, ref)
+        st = dev["stats"]
+        assert 0 < st["kernel_ms_max"] <= st["render_ms_max"] and st["setup_ms"] == 0.0  # plan kept
+    assert m.scene_info()["node_records"] > 0
+    m.close()
+
+
+def test_frame_context_rejects_bad_arguments():
+    import ctypes as C
+    sc = scenes.config("C4", width=32, spp=1)
+    host = g.HostScene(sc.spec)
+    h = C.c_void_p()
+    ids = (C.c_int32 * 1)(0)
+    bad = N.gs_launch(num_gpus=0, tile_w=64, tile_h=64, plan=0, devices=C.cast(ids, C.c_void_p))
+    assert N.lib.gs_multi_create(host.flat_ptr, C.byref(bad), C.byref(h)) == N.GS_ERR_ARG  # devices need num_gpus
+    assert b"device list" in N.lib.gs_last_error()
+    bad = N.gs_launch(num_gpus=2, tile_w=64, tile_h=64, plan=0, devices=None)
+    assert N.lib.gs_multi_create(host.flat_ptr, C.byref(bad), C.byref(h)) == N.GS_ERR_ARG  # one GPU visible
+    ok = N.gs_launch(num_gpus=1, tile_w=64, tile_h=64, plan=0, devices=None)
+    N.check(N.lib.gs_multi_create(host.flat_ptr, C.byref(ok), C.byref(h)))
+    cam = g.camera(sc.camera)
+    cam.image_width = 0
+    assert N.lib.gs_multi_render(h, C.byref(cam), C.byref(sc.settings), 1, None, None) == N.GS_ERR_ARG
+    s = C.c_void_p()
+    assert N.lib.gs_multi_scene(h, 1, C.byref(s)) == N.GS_ERR_ARG
+    N.check(N.lib.gs_multi_destroy(h))
+    host.close()
 
 
 def test_render_multi_ppm_equals_render_ppm():
@@ -83,6 +181,24 @@ def test_bench_gather_over_rccl_one_rank(tmp_path):
     d = json.loads(line[0])
     assert d["config"]["collective"] == "rccl"
     assert np.array_equal(np.load(one), np.load(two))
+
+
+def test_bench_context_path_and_too_many_gpus(tmp_path):
+    """bench.py without a launcher drives the devices through the frame context: its frame
+    equals the one-shot render; --gpus above the visible devices fails with a message."""
+    out = tmp_path / "ctx.npy"
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--no-cpu", "--width", "160",
+                        "--spp", "8", "--seed", "3", "--dump", str(out)], cwd=ROOT, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 1 and d["config"]["collective"] == "none" and "gs_multi" in d["config"]["launch"]
+    assert d["roofline"]["kernel_ms"] > 0 and d["config"]["scene"]["node_records"] > 0
+    ref, _ = g.render(scenes.config("C4", width=160, spp=8), seed=3)
+    assert np.array_equal(np.load(out), ref)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "64", "--steps", "1", "--no-cpu"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "visible" in r.stderr
 
 
 def test_concurrent_launches_of_one_scene():

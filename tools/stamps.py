@@ -42,6 +42,10 @@ def main():
         100.0 * node_clk / max(1, node_clk + leaf_clk), 100.0 * leaf_clk / max(1, node_clk + leaf_clk)))
     print("leaf passes: %.2f distinct refs, %.2f distinct ref kinds per pass" % (
         dist_ref / max(1, it_leaf), dist_kind / max(1, it_leaf)))
+    gvis, wsteps, wsteps_g, wlanes = dbg[19:23].cpu().tolist()
+    print("node steps: %d wave steps (%.1f active lanes), %.1f%% with a lane reading global memory; "
+          "%.1f%% of lane node visits from global memory" % (
+              wsteps, wlanes / max(1, wsteps), 100.0 * wsteps_g / max(1, wsteps), 100.0 * gvis / max(1, wlanes)))
     reg = dbg[10:15].cpu().tolist()
     # split shading (no GS_FEAT_MIXED) stamps background / reconstruct / scatter on their own;
     # staged shading (GS_FEAT_MIXED, media, nested) stamps all of it as region 2
