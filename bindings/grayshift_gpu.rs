@@ -25,7 +25,7 @@ pub const GS_REF_TRIANGLE: u32 = 5;
 pub const GS_REF_LIST: u32 = 6;
 pub const GS_REF_INSTANCE: u32 = 7;
 pub const GS_REF_MEDIUM: u32 = 8;
-pub const GS_ABI_VERSION: i32 = 6;
+pub const GS_ABI_VERSION: i32 = 7;
 pub const fn gs_make_ref(kind: u32, idx: u32) -> u32 { (kind << GS_REF_SHIFT) | (idx & 0x0FFF_FFFF) }
 
 #[repr(C)] #[derive(Clone, Copy, Default)]
@@ -138,6 +138,7 @@ pub struct gs_stats {
 pub struct gs_scene_info {
     pub node_records: u32, pub leaf_records: u32, pub lds_nodes: u32, pub lds_leaves: u32, pub lds_quads: u32,
     pub feat: i32, pub node_steps: i32, pub cert_boxes: i32, pub nodes_per_leaf: f64, pub other_leaf_frac: f64,
+    pub placement: i32, pub pad: i32, pub pilot_ms: f64,
 }
 
 #[link(name = "grayshift")]
@@ -147,6 +148,10 @@ extern "C" {
     pub fn gs_set_tuning(shade_batch: i32, blocks_per_cu: i32, leaf_batch: i32, sample_chunk: i32) -> gs_status;
     pub fn gs_debug_set_partial_budget(bytes: u64) -> gs_status;
     pub fn gs_set_node_steps(node_steps: i32) -> gs_status;
+    pub fn gs_set_placement(mode: i32) -> gs_status;
+    pub fn gs_debug_record_visits(scene: *const gs_device_scene, cam: *const gs_camera, ss: *const gs_sample_settings,
+                                  seed: u64, part: *const gs_partition, d_packed_rgb: *mut f32, d_visits: *mut u32,
+                                  stream: *mut c_void) -> gs_status;
     pub fn gs_device_scene_create(scene: *const gs_flat_scene, out: *mut *mut gs_device_scene) -> gs_status;
     pub fn gs_device_scene_destroy(scene: *mut gs_device_scene) -> gs_status;
     pub fn gs_device_scene_info(scene: *const gs_device_scene, out: *mut gs_scene_info) -> gs_status;

@@ -30,8 +30,11 @@
 #include <cstdio>
 #include <cmath>
 #include <cstring>
+#include <atomic>
+#include <chrono>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../../include/grayshift_gpu.h"
@@ -57,10 +60,10 @@ using namespace gsd;
 #define GS_MIN_WAVES 4
 #endif
 #define GS_MAX_CHAIN 4
-#define GS_NESTED_STACK 32  // max depth of a BVH under a Translate/RotateY chain
+#define GS_NESTED_STACK 32  // max depth of a BVH under a Translate/RotateY chain (validation bound: the walk is stackless)
 // Kernel feature flags (template argument): scenes without them compile the code out.
 #define GS_FEAT_MEDIA 1   // ConstantMedium leaves (RNG draws inside traversal)
-#define GS_FEAT_NESTED 2  // BVHs under Translate/RotateY (a second-level walk, private stack)
+#define GS_FEAT_NESTED 2  // BVHs under Translate/RotateY (a second-level threaded walk)
 #define GS_FEAT_LEAFRUN 4 // sphere leaves come in adjacent pairs: leaf passes test runs of them
 #define GS_FEAT_LDSTREE 8 // every record of the threaded tree is in the LDS mirror: no global path
                           // (instantiated without media / nested BVHs only; C3 +1%, C5 +2.5%)
@@ -68,6 +71,9 @@ using namespace gsd;
                           // staged shading (shade), else one branch per case (shade_split);
                           // media / nested-BVH scenes always stage.  MI355X: C4 +2.2%, C5 +1.6%
                           // staged, C3 (Lambertian + light) -2.8% staged
+#define GS_FEAT_VISITS 32 // count tests per threaded record (the placement pilot, run_pilot)
+// The pilot's instantiation: every code path (any scene), plus the counts.
+#define GS_FEAT_PILOT (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_VISITS)
 
 // ---------------------------------------------------------------- device layout
 // Internal layouts (may differ from the ABI records; converted at upload).
@@ -152,6 +158,10 @@ struct KParams {
     unsigned long long* counters;
     uint32_t* queue;
     uint32_t* item_visits;  // diagnostic: node visits per packed pixel (nullable)
+    // GS_FEAT_VISITS launches (the placement pilot): tests per node record position, then
+    // per leaf record position from visit_leaf_base
+    uint32_t* visits;
+    uint32_t visit_leaf_base, pad1;
 };
 
 // Hot kernel arguments: what the traversal loop reads every step.
@@ -482,35 +492,28 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
 
 // A BVH under a Translate/RotateY chain (final_scene's rotated box of balls, main.rs:
 // 741-755): BVHNode::hit (BVH.rs:69-90) on the ray in the instance's space, as the same
-// left-first walk with a shrinking closest t as the top level, on a private stack.
-// `root`: a device node ref.  Leaves are lists or primitives (validated on the host).
+// left-first walk with a shrinking closest t as the top level.  Like the top level, the
+// nested tree is threaded on the host: its pre-order records (one per node, one per leaf
+// occurrence; DNode with pad0 = 1 for a leaf) with a hit / next link (`left`) and a miss
+// link (`right`; a leaf's `right` is its ABI ref), so the walk is `cur = hit ? left :
+// right` with no stack (round 2's private stack cost these instantiations 216 B/lane of
+// scratch).  `root`: the tree's first record.  Leaves are lists or primitives (validated).
 __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs, uint32_t root, const Ray& r, double tmin,
                                            double closest, uint32_t inst_ref, LeafHit& res,
                                            unsigned long long* cnt) {
     // AABB::hit's `1.0 / ray.direction[axis]` (AABB.rs:64), hoisted per ray (same value)
     const d3 inv = mk(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
-    uint32_t stk[GS_NESTED_STACK];
-    uint32_t sp = 0, cur = root;
+    uint32_t cur = root;
 #pragma unroll 1
-    for (;;) {
-        if (cur == DREF_NONE) {
-            if (sp == 0) break;
-            cur = stk[--sp];
-            continue;
-        }
-        if (cur < DREF_LEAF) {
-            atomicAdd(&cnt[C_NODES], 1ull);
-            const DNode n = ld_node_g(sc.nodes + cur);
-            if (box_hit_v(n, r.o, inv, tmin, closest)) {
-                if (n.right != DREF_NONE) stk[sp++] = n.right;
-                cur = n.left;
-            } else {
-                cur = DREF_NONE;
-            }
-        } else {
-            shape_test<false>(sc, qs, cur, r, tmin, closest, inst_ref, res, cnt);
+    while (cur != THR_END) {
+        const DNode n = ld_node_g(sc.nodes + cur);
+        if (n.pad0) {  // a leaf occurrence: test it, then the next record
+            shape_test<false>(sc, qs, n.right, r, tmin, closest, inst_ref, res, cnt);
             if (res.hit) closest = res.t;  // res.t only ever shrinks
-            cur = DREF_NONE;
+            cur = n.left;
+        } else {
+            atomicAdd(&cnt[C_NODES], 1ull);
+            cur = box_hit_v(n, r.o, inv, tmin, closest) ? n.left : n.right;
         }
     }
 }
@@ -1049,6 +1052,11 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t tid = threadIdx.x;
     const double tmin = 0.001;
+#ifndef GS_NESTED_SITES
+#define GS_NESTED_SITES 1
+#endif
+    // BVHs under instances keep round 1's advance / begin_ray sites (see the shade pass)
+    constexpr bool kOldSites = GS_NESTED_SITES && (FEAT & GS_FEAT_NESTED) != 0;
 #define LD(k) s_d[(k) * GS_BLOCK + tid]
 #define LI(k) s_i[(k) * GS_BLOCK + tid]
 
@@ -1313,13 +1321,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                             LI(L_SAMPLE) = 0u;
                         }
                         st = S_CAM;
-                        if constexpr ((FEAT & GS_FEAT_NESTED) != 0) advance();  // (see the shade pass)
+                        if constexpr (kOldSites) advance();  // (see the shade pass)
                     }
                 }
             }
             need = __builtin_amdgcn_ballot_w64(st == S_NEED);
         }
-        if constexpr ((FEAT & GS_FEAT_NESTED) != 0) break;
+        if constexpr (kOldSites) break;
         if (st == S_CAM) {
             GS_MARK("adv_begin");
             advance();
@@ -1397,6 +1405,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     u32x4 ra, rb;
                     load_tnode<(FEAT & GS_FEAT_LDSTREE) != 0>(s_nodes, A.tnodes, cur, A.lds_nodes << 5, ra, rb);
                     c_nodes++;
+                    if constexpr ((FEAT & GS_FEAT_VISITS) != 0) atomicAdd(&P->visits[cur >> 5], 1u);
                     bool h;
                     if (wave_fast) {
                         bool undecided;
@@ -1459,6 +1468,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 uint32_t next, ref;
                 load_tleaf<(FEAT & GS_FEAT_LDSTREE) != 0>(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr,
                                                          next, ref);
+                if constexpr ((FEAT & GS_FEAT_VISITS) != 0)
+                    atomicAdd(&P->visits[P->visit_leaf_base + (cur & ~THR_LEAF)], 1u);
 #ifdef GS_STAMPS
                 {  // counted by the pass's first active lane (summed over lanes at the end)
                     const uint64_t act = __builtin_amdgcn_ballot_w64(true);
@@ -1519,6 +1530,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     load_tleaf<(FEAT & GS_FEAT_LDSTREE) != 0>(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr,
                                                          next, ref);
                     if ((ref >> GS_REF_SHIFT) != GS_REF_SPHERE) break;
+                    if constexpr ((FEAT & GS_FEAT_VISITS) != 0)
+                        atomicAdd(&P->visits[P->visit_leaf_base + (cur & ~THR_LEAF)], 1u);
                     c_sph++;
                     double t;
                     if (sphere_accept(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
@@ -1622,7 +1635,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             if (ends) {  // the sample is done; its item's next camera ray comes at the loop head
                 GS_STAMP(r0);
                 add_sample(Lr, Lg, Lb);
-                if constexpr ((FEAT & GS_FEAT_NESTED) != 0) {
+                if constexpr (kOldSites) {
                     // BVHs under instances keep round 1's two advance sites (refill and
                     // here): with the single site these instantiations spilled 344-376
                     // B/lane instead of 236 and final_scene ran 16% slower
@@ -1634,7 +1647,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 GS_REGION(4, r0);
             }
         }
-        if constexpr ((FEAT & GS_FEAT_NESTED) != 0) {  // (round 1's begin_ray site too)
+        if constexpr (kOldSites) {  // (round 1's begin_ray site too)
             if (fresh) {
                 begin_ray();
                 fresh = false;
@@ -1767,6 +1780,7 @@ static int64_t lds_mirror_budget() {
 // 16 -> 648.3, 32 -> 647.3; N=8: 4 -> 89.6, 8 -> 89.6, 16 -> 89.7, 32 -> 95.8 (max of the
 // two ranks).  16 is within noise of the best at both ends.
 static int32_t g_sample_chunk = -1;
+static int32_t g_placement = 1;  // 1: placement pilot at a scene's first launch; 0: the static estimate only
 static uint64_t g_partial_budget = 4ull << 30;  // auto chunks: at most 4 GiB of chunk sums (per launch slot)
 
 extern "C" void gs_set_last_error(const char* msg) { tl_err = msg ? msg : ""; }
@@ -1795,6 +1809,15 @@ struct LaunchSlot {
 };
 static const int kLaunchSlots = 4;
 
+// The threaded top-level tree before placement: pre-order records (DNode: a node's f64
+// box, hit link = the next record, miss link; a leaf's sphere inline, next link, ABI ref),
+// with each record's depth and static visit estimate.
+struct ThreadedTree {
+    std::vector<DNode> rec;
+    std::vector<uint8_t> leaf;
+    std::vector<uint32_t> depth;
+    std::vector<double> score;
+};
 struct gs_device_scene {
     int device = 0;
     void* mem = nullptr;  // one allocation for every array
@@ -1829,6 +1852,15 @@ struct gs_device_scene {
     int cus = 0;
     LaunchSlot slots[kLaunchSlots];
     uint32_t next_slot = 0;
+    // Placement of the threaded records (place_records): the static estimate until the
+    // first launch, whose pilot (run_pilot) measures the visits and re-places them.
+    ThreadedTree tree;
+    std::vector<uint32_t> pos;  // tree record -> position (current placement)
+    uint32_t n_quads = 0;
+    int64_t mirror_budget = 0;
+    std::atomic<int> placement{0};  // 0 static, pilot pending; 1 static (final); 2 measured
+    double pilot_ms = 0.0;
+    std::mutex place_mu;  // held while a pilot runs and the records are re-placed
 };
 
 namespace {
@@ -1842,6 +1874,85 @@ struct Layout {
         return off;
     }
 };
+
+// The device arrays of one placement: node records, their f64 boxes, leaf records, with
+// the mirrored prefixes first, and the root's link.
+struct Placed {
+    std::vector<TNode> tnodes;
+    std::vector<TBox> tboxes;
+    std::vector<TLeaf> tleaves;
+    std::vector<uint32_t> pos;  // tree record -> its position in tnodes / tleaves
+    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, root = THR_END;
+};
+#ifndef GS_LDS_LEAVES
+#define GS_LDS_LEAVES 1  // 0: mirror node records only
+#endif
+// Order the records by how likely a ray tests them and fill the block's LDS byte budget in
+// that order (32-B node records, 48-B leaf records; quads take the rest).  `visits` (one
+// count per record, nullable): measured by a pilot launch (GS_FEAT_VISITS), ranked by
+// visits per byte, which maximises the visits the mirror serves; the static estimate
+// orders the unvisited and serves when there is no pilot.  Records outside the mirror
+// stay in pre-order.
+static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* visits, uint32_t n_quads,
+                            int64_t budget) {
+    const uint32_t n = (uint32_t)t.rec.size();
+    Placed out;
+    std::vector<uint32_t> order(n), pos(n);
+    for (uint32_t i = 0; i < n; i++) order[i] = i;
+    auto rec_bytes = [&](uint32_t i) { return t.leaf[i] ? (int64_t)sizeof(TLeaf) : (int64_t)sizeof(TNode); };
+    auto static_first = [&](uint32_t a, uint32_t b) {
+        return t.score[a] > t.score[b] || (t.score[a] == t.score[b] && t.depth[a] < t.depth[b]);
+    };
+    if (visits) {
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+            // compare visits_a / bytes_a with visits_b / bytes_b exactly (integers)
+            const unsigned __int128 va = (unsigned __int128)(*visits)[a] * (uint64_t)rec_bytes(b);
+            const unsigned __int128 vb = (unsigned __int128)(*visits)[b] * (uint64_t)rec_bytes(a);
+            if (va != vb) return va > vb;
+            return static_first(a, b);
+        });
+    } else {
+        std::stable_sort(order.begin(), order.end(), static_first);
+    }
+    std::vector<uint8_t> top(n, 0);
+    int64_t used = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t r = order[i];
+        if (!GS_LDS_LEAVES && t.leaf[r]) continue;
+        const int64_t sz = rec_bytes(r);
+        if (used + sz > budget) {
+            if (used + (int64_t)sizeof(TNode) > budget) break;
+            continue;
+        }
+        used += sz;
+        top[r] = 1;
+        (t.leaf[r] ? out.lds_leaves : out.lds_nodes)++;
+    }
+    out.lds_quads = (uint32_t)std::min<int64_t>(n_quads, std::max<int64_t>(0, budget - used) / (int64_t)sizeof(TQuad));
+    uint32_t nt = 0, nl = 0, nt_rest = out.lds_nodes, nl_rest = out.lds_leaves;
+    for (uint32_t i = 0; i < n; i++) {
+        if (t.leaf[i]) pos[i] = top[i] ? nl++ : nl_rest++;
+        else pos[i] = top[i] ? nt++ : nt_rest++;
+    }
+    out.tnodes.resize(nt_rest);
+    out.tboxes.resize(nt_rest);
+    out.tleaves.resize(nl_rest);
+    auto tag = [&](uint32_t l) { return l >= n ? THR_END : (t.leaf[l] ? (THR_LEAF | pos[l]) : pos[l] << 5); };
+    for (uint32_t i = 0; i < n; i++) {
+        const DNode& r = t.rec[i];
+        if (t.leaf[i]) {
+            out.tleaves[pos[i]] = TLeaf{r.mnx, r.mny, r.mnz, r.mxx, tag(r.left), r.right, 0u, 0u};
+        } else {
+            // f32 box coordinates rounded to nearest (the certified test's error model)
+            out.tnodes[pos[i]] = TNode{(float)r.mnx, (float)r.mny, (float)r.mxx, (float)r.mxy, (float)r.mnz,
+                                       (float)r.mxz, tag(r.left), tag(r.right)};
+            out.tboxes[pos[i]] = TBox{r.mnx, r.mny, r.mnz, r.mxx, r.mxy, r.mxz};
+        }
+    }
+    out.root = n == 0 ? THR_END : tag(0);
+    out.pos = std::move(pos);
+    return out;
+}
 
 // Host-side validation of everything the kernel indexes, so a malformed scene is an
 // error code, never a GPU fault.
@@ -2064,6 +2175,12 @@ gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf
     return GS_OK;
 }
 
+gs_status gs_set_placement(int32_t mode) {
+    if (mode != 0 && mode != 1) return fail(GS_ERR_ARG, "placement mode is 0 or 1");
+    g_placement = mode;
+    return GS_OK;
+}
+
 gs_status gs_debug_set_partial_budget(uint64_t bytes) {
     g_partial_budget = bytes ? bytes : (4ull << 30);
     return GS_OK;
@@ -2079,11 +2196,50 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GS_ERR_NO_DEVICE, "no HIP device visible");
 
-    std::vector<DNode> nodes(s->n_nodes);
-    for (uint32_t i = 0; i < s->n_nodes; i++) {
-        const gs_node& n = s->nodes[i];
-        nodes[i] = DNode{n.min[0], n.min[1], n.min[2], n.max[0], n.max[1], n.max[2],
-                         device_ref(n.left), device_ref(n.right), 0, 0};
+    // BVHs under instance chains (nested_bvh): each distinct root threaded once into
+    // `nodes` (pre-order records: node {box, hit = next record, miss = after its subtree,
+    // pad0 = 0}, leaf {next, ABI ref, pad0 = 1}; THR_END ends a tree), and the device copy
+    // of the instances points its node children at their tree's first record.
+    std::vector<DNode> nodes;
+    std::vector<gs_instance> insts(s->instances, s->instances + s->n_instances);
+    {
+        std::unordered_map<uint32_t, uint32_t> start;  // node index -> first record
+        for (gs_instance& in : insts) {
+            if ((in.child >> GS_REF_SHIFT) != GS_REF_NODE) continue;
+            const uint32_t root = in.child & GS_REF_MASK;
+            auto it = start.find(root);
+            if (it == start.end()) {
+                const uint32_t first = (uint32_t)nodes.size();
+                std::vector<std::pair<uint32_t, bool>> work{{in.child, false}};
+                while (!work.empty()) {
+                    auto [x, close] = work.back();
+                    work.pop_back();
+                    if (close) {
+                        nodes[x].right = (uint32_t)nodes.size();
+                        continue;
+                    }
+                    const uint32_t idx = (uint32_t)nodes.size();
+                    if ((x >> GS_REF_SHIFT) == GS_REF_NODE) {
+                        const gs_node& n = s->nodes[x & GS_REF_MASK];
+                        nodes.push_back(DNode{n.min[0], n.min[1], n.min[2], n.max[0], n.max[1], n.max[2], idx + 1u, 0u,
+                                              0u, 0u});
+                        work.push_back({idx, true});
+                        if (n.right != GS_REF_NONE) work.push_back({n.right, false});
+                        work.push_back({n.left, false});
+                    } else {
+                        nodes.push_back(DNode{0, 0, 0, 0, 0, 0, idx + 1u, x, 1u, 0u});
+                    }
+                }
+                const uint32_t end = (uint32_t)nodes.size();
+                for (uint32_t k = first; k < end; k++) {
+                    if (nodes[k].left == end) nodes[k].left = THR_END;
+                    if (!nodes[k].pad0 && nodes[k].right == end) nodes[k].right = THR_END;
+                }
+                it = start.emplace(root, first).first;
+            }
+            in.child = GS_MAKE_REF(GS_REF_NODE, it->second);
+        }
+        if (nodes.size() > GS_REF_MASK) return fail(GS_ERR_UNSUPPORTED, "more than 2^28 nested BVH records");
     }
     // The threaded top-level tree (see THR_END): pre-order records of nodes and leaf
     // occurrences; raw links first, then split into node and leaf arrays.
@@ -2093,6 +2249,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     std::vector<TBox> tboxes;
     std::vector<TLeaf> tleaves;
     uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, thr_root_tagged = THR_END;
+    ThreadedTree tree_keep;  // kept by the scene: re-placed after a launch's pilot (place_records)
+    std::vector<uint32_t> placed_pos;
     double nodes_per_leaf = 0.0, other_leaf_frac = 0.0;
     bool leaf_runs = false;
     int32_t auto_node_steps = GS_NODE_STEPS;
@@ -2133,13 +2291,14 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         }
         const uint32_t n = (uint32_t)thr.size();
         // Placement: the records a ray is most likely to test first, so a block can mirror
-        // them in LDS; the rest in pre-order.  Likelihood ~ the smallest surface area of a
-        // box on the record's path from the root (a ray tests a record only if it hit all
-        // of them), ties broken by depth (measured on MI355X C4: +1.4% over pure depth
-        // order).  Links are explicit, so placement does not change the walk.
-        std::vector<uint32_t> pos(n);
+        // them in LDS; the rest in pre-order.  Static estimate (until a launch's pilot
+        // measures the real visits, place_records): the smallest surface area of a box on
+        // the record's path from the root (a ray tests a record only if it hit all of
+        // them), ties broken by depth.  Links are explicit, so placement does not change
+        // the walk.
+        std::vector<uint32_t> depth(n, 0);
+        std::vector<double> score(n, 0.0);
         {
-            std::vector<uint32_t> depth(n, 0), order;
             for (uint32_t i = 0; i < n; i++)
                 if (!thr_leaf[i]) {
                     // records are pre-order: a node's descendants follow it, so depths
@@ -2149,10 +2308,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                         c = thr_leaf[c] ? c + 1 : thr[c].right;  // next child of node i
                     }
                 }
-            order.resize(n);
-            for (uint32_t i = 0; i < n; i++) order[i] = i;
             // score = surface area of the parent's box (the chance a ray tests the record)
-            std::vector<double> score(n, 0.0);
             if (n) score[0] = 1e308;
             for (uint32_t i = 0; i < n; i++)
                 if (!thr_leaf[i]) {
@@ -2164,9 +2320,6 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                         c = thr_leaf[c] ? c + 1 : thr[c].right;
                     }
                 }
-            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-                return score[a] > score[b] || (score[a] == score[b] && depth[a] < depth[b]);
-            });
             // Expected node tests per leaf test (the score over the root box's area is the
             // chance a ray entering the root tests the record).
             if (n && !thr_leaf[0]) {
@@ -2184,50 +2337,18 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             } else if (n) {
                 other_leaf_frac = (thr[0].right >> GS_REF_SHIFT) != GS_REF_SPHERE ? 1.0 : 0.0;
             }
-            // Fill the LDS byte budget in that order (32-B node records, 48-B leaf records).
-            const int64_t budget = g_lds_mirror < 0 ? lds_mirror_budget() : g_lds_mirror;
-            std::vector<uint8_t> top(n, 0);
-            int64_t used = 0;
-#ifndef GS_LDS_LEAVES
-#define GS_LDS_LEAVES 1  // 0: mirror node records only
-#endif
-            for (uint32_t i = 0; i < n; i++) {
-                const uint32_t r = order[i];
-                if (!GS_LDS_LEAVES && thr_leaf[r]) continue;
-                const int64_t sz = thr_leaf[r] ? (int64_t)sizeof(TLeaf) : (int64_t)sizeof(TNode);
-                if (used + sz > budget) {
-                    if (used + (int64_t)sizeof(TNode) > budget) break;
-                    continue;
-                }
-                used += sz;
-                top[r] = 1;
-                (thr_leaf[r] ? lds_leaves : lds_nodes)++;
-            }
-            // Quads (a prefix in gs_quad order) take what the tree leaves of the budget.
-            lds_quads = (uint32_t)std::min<int64_t>(s->n_quads,
-                                                    std::max<int64_t>(0, budget - used) / (int64_t)sizeof(TQuad));
-            uint32_t nt = 0, nl = 0, nt_rest = lds_nodes, nl_rest = lds_leaves;
-            for (uint32_t i = 0; i < n; i++) {
-                if (thr_leaf[i]) pos[i] = top[i] ? nl++ : nl_rest++;
-                else pos[i] = top[i] ? nt++ : nt_rest++;
-            }
-            tnodes.resize(nt_rest);
-            tboxes.resize(nt_rest);
-            tleaves.resize(nl_rest);
         }
-        auto tag = [&](uint32_t l) { return l >= n ? THR_END : (thr_leaf[l] ? (THR_LEAF | pos[l]) : pos[l] << 5); };
-        for (uint32_t i = 0; i < n; i++) {
-            const DNode& r = thr[i];
-            if (thr_leaf[i]) {
-                tleaves[pos[i]] = TLeaf{r.mnx, r.mny, r.mnz, r.mxx, tag(r.left), r.right, 0u, 0u};
-            } else {
-                // f32 box coordinates rounded to nearest (the certified test's error model)
-                tnodes[pos[i]] = TNode{(float)r.mnx, (float)r.mny, (float)r.mxx, (float)r.mxy, (float)r.mnz,
-                                       (float)r.mxz, tag(r.left), tag(r.right)};
-                tboxes[pos[i]] = TBox{r.mnx, r.mny, r.mnz, r.mxx, r.mxy, r.mxz};
-            }
-        }
-        thr_root_tagged = n == 0 ? THR_END : tag(0);
+        tree_keep = ThreadedTree{thr, thr_leaf, std::move(depth), std::move(score)};
+        const Placed pl = place_records(tree_keep, nullptr, s->n_quads,
+                                        g_lds_mirror < 0 ? lds_mirror_budget() : g_lds_mirror);
+        tnodes = pl.tnodes;
+        tboxes = pl.tboxes;
+        tleaves = pl.tleaves;
+        lds_nodes = pl.lds_nodes;
+        lds_leaves = pl.lds_leaves;
+        lds_quads = pl.lds_quads;
+        thr_root_tagged = pl.root;
+        placed_pos = pl.pos;
         // Leaf runs pay when at least a quarter of the leaf records are the first of two
         // adjacent sphere leaves (C4's two-sphere leaves of BVH.rs:44-55: ~half).
         {
@@ -2324,7 +2445,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     size_t o_tri = L.add(s->triangles, s->n_triangles * sizeof(gs_triangle));
     size_t o_list = L.add(s->lists, s->n_lists * sizeof(gs_list));
     size_t o_lref = L.add(s->list_refs, s->n_list_refs * 4);
-    size_t o_inst = L.add(s->instances, s->n_instances * sizeof(gs_instance));
+    size_t o_inst = L.add(insts.data(), insts.size() * sizeof(gs_instance));
     size_t o_media = L.add(s->media, s->n_media * sizeof(gs_medium));
     size_t o_perm = L.add(s->noise_perm, s->noise_perm ? s->n_noise_perm : 0);
     size_t o_mat = L.add(mats.data(), mats.size() * sizeof(DMaterial));
@@ -2408,6 +2529,10 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     }
     ds->cert_boxes = cert_boxes;
     ds->node_steps = auto_node_steps;
+    ds->tree = std::move(tree_keep);
+    ds->pos = std::move(placed_pos);
+    ds->n_quads = s->n_quads;
+    ds->mirror_budget = g_lds_mirror < 0 ? lds_mirror_budget() : g_lds_mirror;
     *out = ds;
     return GS_OK;
 }
@@ -2425,6 +2550,8 @@ gs_status gs_device_scene_info(const gs_device_scene* ds, gs_scene_info* out) {
     i.cert_boxes = ds->cert_boxes ? 1 : 0;
     i.nodes_per_leaf = ds->nodes_per_leaf;
     i.other_leaf_frac = ds->other_leaf_frac;
+    i.placement = ds->placement.load(std::memory_order_acquire);
+    i.pilot_ms = ds->pilot_ms;
     *out = i;
     return GS_OK;
 }
@@ -2441,6 +2568,18 @@ gs_status gs_device_scene_destroy(gs_device_scene* ds) {
     if (ds->mem) (void)hipFree(ds->mem);
     delete ds;
     return GS_OK;
+}
+
+// Compute units of a device (cached: the attribute query costs ~0.5 ms).
+static int device_cus(int dev) {
+    static std::atomic<int> cache[64];
+    if (dev < 0 || dev >= 64) return 256;
+    int v = cache[dev].load(std::memory_order_relaxed);
+    if (v == 0) {
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        cache[dev].store(v, std::memory_order_relaxed);
+    }
+    return v;
 }
 
 static bool part_ok(const gs_camera* cam, const gs_partition* p) {
@@ -2476,6 +2615,7 @@ static void (*kernel_for(int feat))(KArgs) {
         case GS_FEAT_MIXED | GS_FEAT_LDSTREE: return gs_render_kernel<GS_FEAT_MIXED | GS_FEAT_LDSTREE>;
         case GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN:
             return gs_render_kernel<GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN>;
+        case GS_FEAT_PILOT: return gs_render_kernel<GS_FEAT_PILOT>;
         default: return gs_render_kernel<0>;
     }
 }
@@ -2507,9 +2647,28 @@ gs_status gs_render_tiles_ex_async(const gs_device_scene* ds, const gs_camera* c
 // The launch behind gs_render_tiles_ex_async; k_begin / k_end (nullable, timing events of
 // the stream's device) are recorded right around the megakernel, so a caller can time the
 // dominant kernel alone (csrc/host/internal.hpp; the frame context's gs_stats.kernel_ms).
+// A GS_FEAT_VISITS launch's count buffer: node record positions, then leaf positions.
+struct VisitArgs {
+    uint32_t* visits;
+    uint32_t leaf_base;
+};
+static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
+                        const gs_partition* part, const gs_render_outputs* outs, gs_counters* d_counters, void* stream,
+                        hipEvent_t k_begin, hipEvent_t k_end, const VisitArgs* va);
+static gs_status ensure_placement(gs_device_scene* ds, const gs_camera* cam, void* stream);
+
 gs_status gs_render_tiles_timed_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
                                       uint64_t seed, const gs_partition* part, const gs_render_outputs* outs,
                                       gs_counters* d_counters, void* stream, hipEvent_t k_begin, hipEvent_t k_end) {
+    if (!ds || !cam) return fail(GS_ERR_ARG, "null argument");
+    gs_status e = ensure_placement(const_cast<gs_device_scene*>(ds), cam, stream);
+    if (e != GS_OK) return e;
+    return launch(ds, cam, ss, seed, part, outs, d_counters, stream, k_begin, k_end, nullptr);
+}
+
+static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
+                        const gs_partition* part, const gs_render_outputs* outs, gs_counters* d_counters, void* stream,
+                        hipEvent_t k_begin, hipEvent_t k_end, const VisitArgs* va) {
     if (!ds || !cam || !ss || !part || !outs || (!outs->rgb && !outs->rgb8)) return fail(GS_ERR_ARG, "null argument");
     if (!part_ok(cam, part)) return fail(GS_ERR_ARG, "bad partition / image size");
     if (ss->batch_size == 0) return fail(GS_ERR_ARG, "batch_size 0 never terminates (camera.rs:137)");
@@ -2541,8 +2700,16 @@ gs_status gs_render_tiles_timed_async(const gs_device_scene* ds, const gs_camera
         const uint32_t bs = ss->batch_size;
         uint32_t c = g_sample_chunk > 0 ? (uint32_t)g_sample_chunk : std::max<uint32_t>(16u, (bs + 63u) / 64u);
         if ((bs + c - 1) / c > 64u) c = (bs + 63u) / 64u;  // at most 64 chunks per pixel
-        if (g_sample_chunk < 0)
+        if (g_sample_chunk < 0) {
+            // Small frames: smaller chunks until every lane of the device gets ~128 items, so
+            // the frame does not wait on a few long items at its end (MI355X final_scene
+            // 400x400 x 64 spp: chunks of 16 -> 211, 4 -> 549, 1 -> 1007 Msamples/s);
+            // never more than 64 chunks per pixel.
+            const uint64_t lanes = (uint64_t)std::max(1, device_cus(dev)) * GS_BLOCK;
+            while (c > 1 && (bs + c / 2 - 1) / (c / 2) <= 64u && (uint64_t)cap * ((bs + c - 1) / c) < 128u * lanes)
+                c /= 2u;
             while (c < bs && (uint64_t)cap * ((bs + c - 1) / c) * 24u > g_partial_budget) c *= 2u;
+        }
         if (c < bs) {
             chunk = c;
             cpp = (bs + c - 1) / c;
@@ -2563,6 +2730,8 @@ gs_status gs_render_tiles_timed_async(const gs_device_scene* ds, const gs_camera
     kp.out8 = outs->rgb8;
     kp.counters = (unsigned long long*)d_counters;
     kp.item_visits = outs->item_visits;
+    kp.visits = va ? va->visits : nullptr;
+    kp.visit_leaf_base = va ? va->leaf_base : 0u;
     KArgs a{};
     a.tnodes = ds->tnodes;
     a.tboxes = ds->tboxes;
@@ -2675,7 +2844,7 @@ gs_status gs_render_tiles_timed_async(const gs_device_scene* ds, const gs_camera
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(sl.queue, 0, 4, st));
     if (k_begin) HIPCHK(hipEventRecord(k_begin, st));
-    hipLaunchKernelGGL(kernel_for(lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
+    hipLaunchKernelGGL(kernel_for(va ? GS_FEAT_PILOT : lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
     if (k_end) HIPCHK(hipEventRecord(k_end, st));
     if (chunk) {
@@ -2686,6 +2855,93 @@ gs_status gs_render_tiles_timed_async(const gs_device_scene* ds, const gs_camera
     HIPCHK(hipEventRecord(sl.done, st));
     sl.used = true;
     sl.stream = st;
+    return GS_OK;
+}
+
+// Placement pilot.  Before a scene's first launch, when its threaded records do not all
+// fit the LDS mirror: render the launch's camera at 1 spp on a grid of every k-th pixel
+// (k chosen for ~128 k pilot pixels) with the GS_FEAT_VISITS instantiation, which counts
+// the tests of every node and leaf record, then re-place the records by measured visits
+// per byte (place_records) and upload them again.  The static estimate ranks records by
+// geometry alone and misses where the camera's rays actually go (MI355X C4: its mirror
+// served 90.8% of node visits and 50.2% of leaf tests; the measured order of the same
+// bytes serves 99.6% and 96.0%, tools/visitmap.py).  Placement never changes a result
+// (links are explicit), and the pilot is deterministic, so every device of a multi-GPU
+// render places its copy identically.
+static gs_status run_pilot(gs_device_scene* ds, const gs_camera* cam, void* stream) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int64_t px = (int64_t)cam->image_width * cam->image_height;
+    const int32_t k = std::max<int32_t>(1, (int32_t)std::sqrt((double)px / 131072.0));
+    gs_camera pc = *cam;
+    pc.image_width = (cam->image_width + k - 1) / k;
+    pc.image_height = (cam->image_height + k - 1) / k;
+    for (int a = 0; a < 3; a++) {
+        pc.pixel_delta_u[a] = cam->pixel_delta_u[a] * (double)k;
+        pc.pixel_delta_v[a] = cam->pixel_delta_v[a] * (double)k;
+    }
+    gs_partition part{0, 1, 64, 64, nullptr, 0, 0};
+    const int64_t cap = gs_partition_capacity(&pc, &part);
+    const uint32_t nn = ds->node_records, nl = ds->leaf_records;
+    float* d_rgb = nullptr;
+    uint32_t* d_vis = nullptr;
+    if (hipMalloc(&d_rgb, (size_t)cap * 12 + 16) != hipSuccess ||
+        hipMalloc(&d_vis, ((size_t)nn + nl) * 4 + 16) != hipSuccess) {
+        if (d_rgb) (void)hipFree(d_rgb);
+        return fail(GS_ERR_OOM, "hipMalloc of the placement pilot's buffers failed");
+    }
+    hipStream_t st = (hipStream_t)stream;
+    gs_sample_settings one{0.0, 0.0, 1, 0};  // one sample per pixel (camera.rs:158: max_samples < batch)
+    gs_render_outputs o{d_rgb, nullptr, nullptr};
+    VisitArgs va{d_vis, nn};
+    std::vector<uint32_t> vis((size_t)nn + nl);
+    hipError_t e = hipMemsetAsync(d_vis, 0, ((size_t)nn + nl) * 4, st);
+    gs_status r = e == hipSuccess ? launch(ds, &pc, &one, 1, &part, &o, nullptr, stream, nullptr, nullptr, &va)
+                                  : fail(GS_ERR_HIP, hipGetErrorString(e));
+    if (r == GS_OK) {
+        e = hipStreamSynchronize(st);
+        if (e == hipSuccess) e = hipMemcpy(vis.data(), d_vis, vis.size() * 4, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) r = fail(GS_ERR_HIP, std::string("placement pilot: ") + hipGetErrorString(e));
+    }
+    (void)hipFree(d_rgb);
+    (void)hipFree(d_vis);
+    if (r != GS_OK) return r;
+    const ThreadedTree& t = ds->tree;
+    std::vector<uint64_t> counts(t.rec.size());
+    for (size_t i = 0; i < t.rec.size(); i++) counts[i] = t.leaf[i] ? vis[(size_t)nn + ds->pos[i]] : vis[ds->pos[i]];
+    Placed pl = place_records(t, &counts, ds->n_quads, ds->mirror_budget);
+    if (pl.tnodes.size() != nn || pl.tleaves.size() != nl) return fail(GS_ERR_HIP, "placement changed the record counts");
+    // Nothing of this scene runs on the device yet (the pilot was its first launch and has
+    // finished), so the arrays are rewritten in place.
+    HIPCHK(hipMemcpy(const_cast<TNode*>(ds->tnodes), pl.tnodes.data(), pl.tnodes.size() * sizeof(TNode), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(const_cast<TBox*>(ds->tboxes), pl.tboxes.data(), pl.tboxes.size() * sizeof(TBox), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(const_cast<TLeaf*>(ds->tleaves), pl.tleaves.data(), pl.tleaves.size() * sizeof(TLeaf),
+                     hipMemcpyHostToDevice));
+    {
+        std::lock_guard<std::mutex> lock(ds->mu);
+        ds->thr_root = pl.root;
+        ds->lds_nodes = pl.lds_nodes;
+        ds->lds_leaves = pl.lds_leaves;
+        ds->lds_quads = pl.lds_quads;
+        ds->pos = std::move(pl.pos);
+        ds->lcfg[0].ready = ds->lcfg[1].ready = false;  // mirror prefixes changed
+    }
+    ds->pilot_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return GS_OK;
+}
+
+static gs_status ensure_placement(gs_device_scene* ds, const gs_camera* cam, void* stream) {
+    if (ds->placement.load(std::memory_order_acquire) != 0) return GS_OK;
+    std::lock_guard<std::mutex> g(ds->place_mu);
+    if (ds->placement.load(std::memory_order_relaxed) != 0) return GS_OK;
+    const bool all_mirrored = ds->lds_nodes == ds->node_records && ds->lds_leaves == ds->leaf_records;
+    if (!g_placement || all_mirrored || cam->image_width <= 0 || cam->image_height <= 0) {
+        ds->placement.store(1, std::memory_order_release);
+        return GS_OK;
+    }
+    const gs_status r = run_pilot(ds, cam, stream);
+    if (r != GS_OK) return r;  // (tried again at the next launch)
+    ds->tree = ThreadedTree{};  // not needed again
+    ds->placement.store(2, std::memory_order_release);
     return GS_OK;
 }
 
@@ -2759,6 +3015,18 @@ gs_status gs_plan_tiles(const gs_device_scene* ds, const gs_camera* cam, uint64_
             order_out[(size_t)sl * world + rk] = sl < (int32_t)lists[rk].size() ? lists[rk][sl] : -1;
     *slots_per_rank = slots;
     return GS_OK;
+}
+
+gs_status gs_debug_record_visits(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
+                                 uint64_t seed, const gs_partition* part, float* d_packed_rgb, uint32_t* d_visits,
+                                 void* stream) {
+    if (!ds || !cam || !d_packed_rgb || !d_visits) return fail(GS_ERR_ARG, "null argument");
+    gs_status e = ensure_placement(const_cast<gs_device_scene*>(ds), cam, stream);
+    if (e != GS_OK) return e;
+    HIPCHK(hipMemsetAsync(d_visits, 0, ((size_t)ds->node_records + ds->leaf_records) * 4, (hipStream_t)stream));
+    gs_render_outputs o{d_packed_rgb, nullptr, nullptr};
+    VisitArgs va{d_visits, ds->node_records};
+    return launch(ds, cam, ss, seed, part, &o, nullptr, stream, nullptr, nullptr, &va);
 }
 
 gs_status gs_device_alloc(int64_t bytes, void** d_out) {

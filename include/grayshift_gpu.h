@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 6
+#define GS_ABI_VERSION 7
 
 typedef int32_t gs_status;
 enum {
@@ -218,8 +218,9 @@ int32_t gs_version(void);
  * runs a leaf-test pass (0 acts as 1);
  * sample_chunk = samples per work item when the settings run a single batch
  * (max_samples < batch_size, as every fixed-spp render): -1 auto (16, or batch/64 for
- * big batches: at most 64 chunks per pixel, and at most 4 GiB of chunk sums), 0 never
- * split a pixel, n > 0 explicit.
+ * big batches; halved while the launch has fewer than ~128 items per GPU lane, down to 1
+ * (ABI 7: small frames end without a long tail); at most 64 chunks per pixel and at most
+ * 4 GiB of chunk sums), 0 never split a pixel, n > 0 explicit.
  * Chunks keep every sample's RNG stream; a pixel's chunk sums are added in sample order,
  * so only the association of the f64 colour sum differs from the sequential loop. */
 gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf_batch, int32_t sample_chunk);
@@ -228,6 +229,23 @@ gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf
  * up to this many BVH node steps before the wave re-checks which lanes sit at leaves.
  * 0 (default) = the scene's own choice, from its tree's shape at gs_device_scene_create. */
 gs_status gs_set_node_steps(int32_t node_steps);
+
+/* Placement of the threaded BVH records (ABI 7).  1 (default): before a scene's first
+ * launch, when its records do not all fit the per-block LDS mirror, a pilot renders the
+ * launch's camera at 1 spp on a coarse pixel grid counting the tests of every record,
+ * and the records are re-placed so the mirror holds the most-tested bytes (the pilot's
+ * cost is reported as gs_scene_info.pilot_ms; results never depend on placement).
+ * 0: keep the static estimate placed by gs_device_scene_create.  Applies to scenes
+ * whose first launch comes after the call. */
+gs_status gs_set_placement(int32_t mode);
+
+/* Diagnostic (ABI 7): one launch like gs_render_tiles_async that also counts, into the
+ * device array d_visits (node_records + leaf_records u32, zeroed by the call), the tests
+ * of every threaded record by its current position: node records first, then leaf
+ * records.  Runs the scene's placement first, like any launch. */
+gs_status gs_debug_record_visits(const gs_device_scene* scene, const gs_camera* cam,
+                                 const gs_sample_settings* ss, uint64_t seed, const gs_partition* part,
+                                 float* d_packed_rgb, uint32_t* d_visits, void* stream);
 
 /* Test hook: the auto sample-chunk rule's budget for chunk sums (default 4 GiB; 0
  * restores it).  A smaller budget makes renders take the chunk-doubling branch. */
@@ -253,6 +271,10 @@ typedef struct gs_scene_info {
     int32_t cert_boxes; /* every node coordinate |x| <= 1e15: the certified f32 box test applies */
     double nodes_per_leaf;
     double other_leaf_frac;
+    int32_t placement;  /* (ABI 7) 0 static estimate, first launch pending; 1 static estimate (final);
+                           2 measured by the first launch's pilot (gs_set_placement) */
+    int32_t pad;
+    double pilot_ms;    /* (ABI 7) host time of that pilot and re-placement */
 } gs_scene_info;
 gs_status gs_device_scene_info(const gs_device_scene* scene, gs_scene_info* out);
 

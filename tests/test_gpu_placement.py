@@ -1,0 +1,86 @@
+"""Placement of the threaded BVH records in the per-block LDS mirror (render.hip
+place_records / run_pilot): the first launch of a scene whose records do not all fit
+runs a pilot that counts every record's tests and re-places the records by measured
+visits per byte.  Placement must never change a frame or a counter, the pilot's counts
+must be the frame's own work counts, and the re-placed mirror must serve more of the
+visits than the static estimate."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import grayshift_amd as g
+from grayshift_amd import _native as N
+from grayshift_amd import scenes
+
+pytestmark = pytest.mark.gpu
+
+
+class _placement:
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        N.check(N.lib.gs_set_placement(self.mode))
+
+    def __exit__(self, *a):
+        N.check(N.lib.gs_set_placement(1))
+
+
+def _visits(r, torch):
+    dev = torch.device("cuda", 0)
+    info = r.scene_info()
+    nn, nl = info["node_records"], info["leaf_records"]
+    packed = torch.zeros(r.capacity * 3, dtype=torch.float32, device=dev)
+    vm = torch.zeros(nn + nl, dtype=torch.int32, device=dev)
+    N.check(N.lib.gs_debug_record_visits(r.dev, C.byref(r.cam), C.byref(r.settings), 3, C.byref(r.part),
+                                         C.c_void_p(packed.data_ptr()), C.c_void_p(vm.data_ptr()), None))
+    torch.cuda.synchronize()
+    v = vm.cpu().numpy().astype(np.int64)
+    return r.scene_info(), v[:nn], v[nn:], packed.cpu().numpy()
+
+
+@pytest.mark.parametrize("config,width,spp", [("C4", 240, 8), ("C5", 160, 4), ("C2", 96, 8)])
+def test_placement_never_changes_the_frame(config, width, spp):
+    sc = scenes.config(config, width=width, spp=spp)
+    with _placement(0):
+        ref, rc = g.render(sc, seed=11)
+    img, c = g.render(sc, seed=11)
+    assert np.array_equal(img, ref)
+    assert c == rc
+
+
+def test_pilot_places_and_counts_the_frames_work():
+    torch = pytest.importorskip("torch")
+    sc = scenes.config("C4", width=320, spp=4)
+    with _placement(0):
+        r0 = g.Renderer(sc, 0, 1, 64)
+        s_info, s_nodes, s_leaves, s_img = _visits(r0, torch)
+        r0.close()
+    r1 = g.Renderer(sc, 0, 1, 64)
+    m_info, m_nodes, m_leaves, m_img = _visits(r1, torch)
+    r1.close()
+    assert s_info["placement"] == 1 and m_info["placement"] == 2 and m_info["pilot_ms"] > 0
+    # the same frame and the same total work under either placement
+    assert np.array_equal(s_img, m_img)
+    assert s_nodes.sum() == m_nodes.sum() and s_leaves.sum() == m_leaves.sum()
+    assert sorted(s_nodes.tolist()) == sorted(m_nodes.tolist())
+    # the counts are the frame's own counters (C4: top-level nodes only, sphere leaves only)
+    _, c = g.render(sc, seed=3)
+    assert m_nodes.sum() == c["node_visits"] and m_leaves.sum() == c["sphere_tests"]
+    # the measured placement's mirror serves at least as many visits as the static one
+    served = lambda info, n, l: n[:info["lds_nodes"]].sum() + l[:info["lds_leaves"]].sum()
+    assert served(m_info, m_nodes, m_leaves) >= served(s_info, s_nodes, s_leaves)
+    assert m_nodes[:m_info["lds_nodes"]].sum() > 0.97 * m_nodes.sum()
+
+
+def test_whole_tree_scenes_skip_the_pilot():
+    torch = pytest.importorskip("torch")
+    sc = scenes.config("C3", width=64, spp=2)
+    r = g.Renderer(sc, 0, 1, 64)
+    assert r.scene_info()["placement"] == 0  # pending until the first launch
+    info, nodes, leaves, _ = _visits(r, torch)
+    r.close()
+    assert info["lds_nodes"] == info["node_records"] and info["lds_leaves"] == info["leaf_records"]
+    assert info["placement"] == 1 and info["pilot_ms"] == 0.0
+    assert nodes.sum() > 0
