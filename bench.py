@@ -51,13 +51,18 @@ SIMDS = 1024  # 256 CUs x 4 SIMDs
 # Issue cycles per wave64 VALU instruction on one SIMD-32 at full occupancy, by the PMC
 # instruction classes (SQ_INSTS_VALU_*; "OTHER" = SQ_INSTS_VALU minus the listed classes:
 # moves, compares, selects, bit operations, f32 min/max).  MI355X_MICROARCH.md:54,473: a
-# wave64 32-bit VALU instruction issues over 2 cycles on a SIMD-32.  The rest measured by
-# tools/ubench/valu_rate.hip (profiles/r03/valu_rate_ubench.txt: 8 waves/SIMD, SGPR /
-# inline-constant operands, cycles at the in-kernel clock): f64 add / mul / fma and the
-# 64-bit integer ops issue like 32-bit ones; f64 transcendentals (v_sqrt_f64, v_rcp_f64)
-# take 8, f32 ones 2.
-VALU_CYCLES = {"ADD_F32": 2, "MUL_F32": 2, "FMA_F32": 2, "TRANS_F32": 2, "ADD_F64": 2, "MUL_F64": 2,
-               "FMA_F64": 2, "TRANS_F64": 8, "INT32": 2, "INT64": 2, "CVT": 2, "OTHER": 2}
+# wave64 32-bit VALU instruction issues over 2 cycles on a SIMD-32; f64 runs at half the
+# f32 vector rate (4).  tools/ubench/valu_rate.hip (profiles/r03/valu_rate_ubench.txt,
+# 8 waves per SIMD, cycles at the in-kernel clock) measured: 2.2 for VOP1/VOP2 forms with
+# VGPR operands, 4.1 for the 8-byte VOP3 forms (SGPR / constant operands, v_pk_fma_f32,
+# 64-bit integer ops) and every f64 add / mul / fma, 8.1 for v_sqrt_f32, 16.1 for
+# v_sqrt_f64 / v_rcp_f64.  VALU_CYCLES prices the classes at those costs with 32-bit
+# non-transcendental work at the guide's 2 (a lower bound: the kernel's VOP3 share costs
+# 4), so `frac` is the smallest defensible VALU-issue fraction; `frac_vop3` prices every
+# non-transcendental instruction at the measured VOP3 cost of 4 (the upper bound).
+VALU_CYCLES = {"ADD_F32": 2, "MUL_F32": 2, "FMA_F32": 2, "TRANS_F32": 8, "ADD_F64": 4, "MUL_F64": 4,
+               "FMA_F64": 4, "TRANS_F64": 16, "INT32": 2, "INT64": 4, "CVT": 2, "OTHER": 2}
+VALU_CYCLES_VOP3 = {k: max(v, 4) for k, v in VALU_CYCLES.items()}
 PARITY_TOL = 1e-3  # north star: per-channel |delta| < 1e-3 vs the CPU path at a fixed seed
 
 
@@ -334,19 +339,20 @@ def emit(a, sc, r, c, elapsed, kernel_avg_ms, img, world, launch_info):
     print(json.dumps(out), flush=True)
 
 
-def valu_cycles(k):
+def valu_cycles(k, cost=None):
     """Issue cycles of a launch's VALU instructions on their SIMDs: every PMC instruction
-    class times its measured cost (VALU_CYCLES), the unclassified rest at 2 cycles.
+    class times its cost (VALU_CYCLES, or `cost`), the unclassified rest as "OTHER".
     Returns (cycles, {class: [count, cycles]})."""
-    classes = [c for c in VALU_CYCLES if c != "OTHER"]
+    cost = cost or VALU_CYCLES
+    classes = [c for c in cost if c != "OTHER"]
     mix = {}
     listed = 0.0
     for c in classes:
         n = float(k.get("SQ_INSTS_VALU_" + c, 0.0))
         listed += n
-        mix[c] = [n, n * VALU_CYCLES[c]]
+        mix[c] = [n, n * cost[c]]
     other = max(0.0, float(k["SQ_INSTS_VALU"]) - listed)
-    mix["OTHER"] = [other, other * VALU_CYCLES["OTHER"]]
+    mix["OTHER"] = [other, other * cost["OTHER"]]
     return sum(v[1] for v in mix.values()), mix
 
 
@@ -385,10 +391,12 @@ def roofline(a, c, world, kernel_ms, invalid):
     prof_s = pj["kernel_duration_ms_profiled"] / 1e3
     clock = k["GRBM_GUI_ACTIVE"] / 8.0 / prof_s  # effective shader clock of the profiled launch (Hz)
     cyc, mix = valu_cycles(k)
+    cyc4, _ = valu_cycles(k, VALU_CYCLES_VOP3)
     achieved = cyc / kernel_s  # VALU issue cycles per second, all SIMDs
     peak = SIMDS * clock
     wc = float(k.get("SQ_WAVE_CYCLES", 0.0)) or 1.0
     out.update({"achieved": round(achieved / 1e9, 2), "peak": round(peak / 1e9, 2), "frac": round(achieved / peak, 4),
+                "frac_vop3": round(cyc4 / kernel_s / peak, 4),
                 "traffic": pj["hbm_bytes_per_launch"],
                 "hbm_frac": round(pj["hbm_bytes_per_launch"] / kernel_s / 1e9 / HBM_PEAK_GBS, 5),
                 "effective_clock_ghz": round(clock / 1e9, 3),

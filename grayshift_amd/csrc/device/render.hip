@@ -147,10 +147,16 @@ struct KParams {
     // gs_combine_kernel sums a pixel's chunks in chunk order.  chunk == 0: one item per
     // pixel running the reference's batch loop (camera.rs:135-165) to completion.
     uint32_t chunk, cpp, n_items;
+    // Guided tail: the packed pixels from fine_px on (the rank's last tiles in queue order)
+    // run in smaller chunks (fine_chunk samples, fine_cpp per pixel), their items from
+    // fine_base = fine_px * cpp on, so the frame's last items are short (fine_px =
+    // capacity: no fine region).
+    uint32_t fine_px, fine_base, fine_chunk, fine_cpp;
     uint32_t claim;  // work items a wave claims per queue atomic (its private reserve)
+    uint32_t claim_fine;  // the same once the wave's claims reach the fine region
     // multiply-shift forms of the launch's fixed divisors (devmath.hpp UDiv): chunks per
     // pixel, tile pixels, 8x8 blocks per tile row, tile width, tiles per row, image width
-    UDiv u_cpp, u_tpx, u_bpr, u_tw, u_tx, u_w;
+    UDiv u_cpp, u_tpx, u_bpr, u_tw, u_tx, u_w, u_fcpp;
     const int32_t* order;  // position -> tile (gs_partition.d_tile_order), or null: tile = position
     double* partial;
     float* out;     // linear colour per packed pixel (nullable when out8 is set)
@@ -971,6 +977,21 @@ __device__ GS_NOINLINE Scatter scatter(const DevScene& sc, HitRec h, d3 in_dir, 
 
 __device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull << lane) - 1ull; }
 
+// The placement pilot's count (GS_FEAT_VISITS): one atomic per distinct record among the
+// wave's active lanes (every ray of a pilot tests the root and the records below it: one
+// atomic per lane on those addresses serialised the pilot, 111 ms on MI355X C4).
+__device__ __forceinline__ void count_visit(uint32_t* counts, uint32_t idx) {
+    uint64_t m = __builtin_amdgcn_ballot_w64(true);
+#pragma unroll 1
+    while (m != 0) {
+        const uint32_t lead = (uint32_t)__builtin_ctzll(m);
+        const uint32_t v = __builtin_amdgcn_readlane(idx, lead);
+        const uint64_t same = __builtin_amdgcn_ballot_w64(idx == v);
+        if ((threadIdx.x & 63u) == lead) atomicAdd(&counts[v], (uint32_t)__popcll(same));
+        m &= ~same;
+    }
+}
+
 // Diagnostic build only (-DGS_STAMPS): per-wave shader-clock totals of the three loop
 // phases, written to their own debug buffer (the d_item_visits pointer, reinterpreted
 // as u64[3]) — never to an output.  The stamps' fences perturb scheduling, so only the
@@ -1242,14 +1263,15 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             if (res_cnt == 0) {
                 const uint32_t leader = (uint32_t)__ffsll((long long)need) - 1;
                 uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(P->queue, P->claim);
+                const uint32_t cl = res_base >= P->fine_base ? P->claim_fine : P->claim;
+                if (lane == leader) base = atomicAdd(P->queue, cl);
                 base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
                 if (base >= P->n_items) {
                     qdone = true;
                     break;
                 }
                 res_base = base;
-                res_cnt = min(P->claim, P->n_items - base);
+                res_cnt = min(cl, P->n_items - base);
             }
             const uint32_t n = (uint32_t)__popcll(need);
             const uint32_t take = min(n, res_cnt);
@@ -1266,9 +1288,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 } else {
                     // work order: 8x8 blocks inside each tile (coherent primary rays), a
                     // pixel's chunks adjacent
-                    const uint32_t cpp = P->cpp;
                     const uint32_t q32 = (uint32_t)q;  // q < n_items < 2^32
-                    const uint32_t pq = udiv(q32, P->u_cpp), ck = q32 - pq * cpp;
+                    const bool fine = q32 >= P->fine_base;
+                    const uint32_t cpp = fine ? P->fine_cpp : P->cpp, csz = fine ? P->fine_chunk : P->chunk;
+                    const uint32_t qr = fine ? q32 - P->fine_base : q32;
+                    const uint32_t pr = udiv(qr, fine ? P->u_fcpp : P->u_cpp), ck = qr - pr * cpp;
+                    const uint32_t pq = fine ? P->fine_px + pr : pr;
                     const uint32_t slot = udiv(pq, P->u_tpx), w = pq - slot * tile_px;
                     uint32_t x, y;
                     if (blocked8) {
@@ -1307,9 +1332,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         LD(L_CSG) = 0.0;
                         LD(L_CSB) = 0.0;
                         if (P->chunk) {
-                            LI(L_ITEM) = item * cpp + ck;
-                            LI(L_SAMPLE) = ck * P->chunk;
-                            LI(L_BLEFT) = min(P->chunk, P->ss.batch_size - ck * P->chunk);
+                            // chunk sums: a coarse pixel's at item * cpp, a fine one's after
+                            // every coarse pixel's (the packed pixel and its queue position
+                            // share a tile, so both are in the fine region or neither)
+                            LI(L_ITEM) = fine ? P->fine_base + (item - P->fine_px) * cpp + ck : item * cpp + ck;
+                            LI(L_SAMPLE) = ck * csz;
+                            LI(L_BLEFT) = min(csz, P->ss.batch_size - ck * csz);
                             if (ck == 0) atomicAdd(&s_cnt[C_PIX], 1ull);
                         } else {
                             LD(L_LSUM) = 0.0;
@@ -1405,7 +1433,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     u32x4 ra, rb;
                     load_tnode<(FEAT & GS_FEAT_LDSTREE) != 0>(s_nodes, A.tnodes, cur, A.lds_nodes << 5, ra, rb);
                     c_nodes++;
-                    if constexpr ((FEAT & GS_FEAT_VISITS) != 0) atomicAdd(&P->visits[cur >> 5], 1u);
+                    if constexpr ((FEAT & GS_FEAT_VISITS) != 0) count_visit(P->visits, cur >> 5);
                     bool h;
                     if (wave_fast) {
                         bool undecided;
@@ -1468,8 +1496,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 uint32_t next, ref;
                 load_tleaf<(FEAT & GS_FEAT_LDSTREE) != 0>(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr,
                                                          next, ref);
-                if constexpr ((FEAT & GS_FEAT_VISITS) != 0)
-                    atomicAdd(&P->visits[P->visit_leaf_base + (cur & ~THR_LEAF)], 1u);
+                if constexpr ((FEAT & GS_FEAT_VISITS) != 0) count_visit(P->visits, P->visit_leaf_base + (cur & ~THR_LEAF));
 #ifdef GS_STAMPS
                 {  // counted by the pass's first active lane (summed over lanes at the end)
                     const uint64_t act = __builtin_amdgcn_ballot_w64(true);
@@ -1531,7 +1558,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                                                          next, ref);
                     if ((ref >> GS_REF_SHIFT) != GS_REF_SPHERE) break;
                     if constexpr ((FEAT & GS_FEAT_VISITS) != 0)
-                        atomicAdd(&P->visits[P->visit_leaf_base + (cur & ~THR_LEAF)], 1u);
+                        count_visit(P->visits, P->visit_leaf_base + (cur & ~THR_LEAF));
                     c_sph++;
                     double t;
                     if (sphere_accept(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
@@ -1734,9 +1761,11 @@ __global__ void gs_combine_kernel(const KParams* __restrict__ P) {
             }
             continue;
         }
-        const double* p = P->partial + (size_t)k * cpp * 3;
+        const bool fine = k >= P->fine_px;
+        const uint32_t n = fine ? P->fine_cpp : cpp;
+        const double* p = P->partial + (fine ? (size_t)P->fine_base + (size_t)(k - P->fine_px) * n : (size_t)k * cpp) * 3;
         double r = 0.0, g = 0.0, b = 0.0;
-        for (uint32_t c = 0; c < cpp; c++) {
+        for (uint32_t c = 0; c < n; c++) {
             r += p[c * 3];
             g += p[c * 3 + 1];
             b += p[c * 3 + 2];
@@ -2695,31 +2724,55 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     kp.order = part->d_tile_order;
     // Split pixels into sample chunks only when the settings run exactly one batch:
     // max_samples < batch_size makes the first stop test (camera.rs:158) always true.
-    uint32_t chunk = 0, cpp = 1;
+    uint32_t chunk = 0, cpp = 1, fine_px = (uint32_t)cap, fine_chunk = 1, fine_cpp = 1;
     if (g_sample_chunk != 0 && ss->max_samples < ss->batch_size) {
         const uint32_t bs = ss->batch_size;
         uint32_t c = g_sample_chunk > 0 ? (uint32_t)g_sample_chunk : std::max<uint32_t>(16u, (bs + 63u) / 64u);
         if ((bs + c - 1) / c > 64u) c = (bs + 63u) / 64u;  // at most 64 chunks per pixel
-        if (g_sample_chunk < 0) {
-            // Small frames: smaller chunks until every lane of the device gets ~128 items, so
-            // the frame does not wait on a few long items at its end (MI355X final_scene
-            // 400x400 x 64 spp: chunks of 16 -> 211, 4 -> 549, 1 -> 1007 Msamples/s);
-            // never more than 64 chunks per pixel.
-            const uint64_t lanes = (uint64_t)std::max(1, device_cus(dev)) * GS_BLOCK;
-            while (c > 1 && (bs + c / 2 - 1) / (c / 2) <= 64u && (uint64_t)cap * ((bs + c - 1) / c) < 128u * lanes)
-                c /= 2u;
+        if (g_sample_chunk < 0)
             while (c < bs && (uint64_t)cap * ((bs + c - 1) / c) * 24u > g_partial_budget) c *= 2u;
+        if (g_sample_chunk < 0) {
+            // Guided tail: a work item of c samples started just before the queue runs dry
+            // can keep its lane busy for c samples while every other lane idles, and a frame
+            // with few items per lane ends on them (MI355X final_scene 400x400 x 64 spp,
+            // every pixel in chunks of 16: 211 Msamples/s; of 1: 1007).  So the rank's last
+            // tiles in queue order run in the finest chunks (at most 64 per pixel): enough
+            // tiles for 2 x lanes x c samples, which keeps the other lanes busy while the
+            // last coarse items finish.  Pixels with one chunk of all bs samples sum exactly
+            // like the unsplit loop, fine pixels of 1-sample chunks too.
+            c = std::min(c, bs);
+            const uint32_t fc = std::max<uint32_t>(1u, (bs + 63u) / 64u);
+            const uint64_t tile_px = (uint64_t)part->tile_w * part->tile_h, slots = (uint64_t)cap / tile_px;
+            const uint64_t lanes = (uint64_t)std::max(1, device_cus(dev)) * GS_BLOCK;
+            if (fc < c && slots > 0) {
+                const uint64_t want = 2ull * lanes * c;  // samples
+                const uint64_t ft = std::min<uint64_t>(slots, (want + tile_px * bs - 1) / (tile_px * bs));
+                const uint32_t fpx = (uint32_t)((slots - ft) * tile_px), fcpp = (bs + fc - 1) / fc;
+                const uint64_t items = (uint64_t)fpx * ((bs + c - 1) / c) + ((uint64_t)cap - fpx) * fcpp;
+                if (items * 24u <= g_partial_budget && items < 0xFFFFFFFFull) {
+                    fine_px = fpx;
+                    fine_chunk = fc;
+                    fine_cpp = fcpp;
+                }
+            }
         }
-        if (c < bs) {
+        if (c < bs || fine_px < (uint32_t)cap) {
             chunk = c;
             cpp = (bs + c - 1) / c;
         }
     }
-    if ((uint64_t)cap * cpp >= 0xFFFFFFFFull) chunk = 0, cpp = 1;
+    if ((uint64_t)fine_px * cpp + ((uint64_t)cap - fine_px) * fine_cpp >= 0xFFFFFFFFull)
+        chunk = 0, cpp = 1, fine_px = (uint32_t)cap, fine_cpp = 1;
+    if (!chunk) fine_px = (uint32_t)cap, fine_chunk = 1, fine_cpp = 1;
     kp.chunk = chunk;
     kp.cpp = cpp;
-    kp.n_items = (uint32_t)cap * cpp;
+    kp.fine_px = fine_px;
+    kp.fine_base = fine_px * cpp;
+    kp.fine_chunk = fine_chunk;
+    kp.fine_cpp = fine_cpp;
+    kp.n_items = fine_px * cpp + ((uint32_t)cap - fine_px) * fine_cpp;
     kp.u_cpp = udiv_make(cpp);
+    kp.u_fcpp = udiv_make(fine_cpp);
     kp.u_tpx = udiv_make((uint32_t)(part->tile_w * part->tile_h));
     kp.u_bpr = udiv_make(std::max<uint32_t>(1, (uint32_t)part->tile_w >> 3));
     kp.u_tw = udiv_make((uint32_t)part->tile_w);
@@ -2795,9 +2848,13 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     // ends holding at most one partly used reserve), at least 1.
     const uint64_t waves = (uint64_t)blocks * (GS_BLOCK / 64);
     kp.claim = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, (uint64_t)kp.n_items / waves / 8));
+#ifndef GS_CLAIM_FINE
+#define GS_CLAIM_FINE 128  // MI355X C1 (1-2 sample items): 32 -> 6786, 128 -> 12397, 512 -> 12559; perlin 3169, 3221, 2670
+#endif
+    kp.claim_fine = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(GS_CLAIM_FINE, (uint64_t)kp.n_items / waves / 8));
     // The u32 queue counter runs past n_items by at most one claim per wave (each wave's
     // last, failed claim): it must not wrap.
-    if ((uint64_t)kp.n_items + (uint64_t)kp.claim * (waves + 1) >= 0xFFFFFFFFull)
+    if ((uint64_t)kp.n_items + (uint64_t)std::max(kp.claim, kp.claim_fine) * (waves + 1) >= 0xFFFFFFFFull)
         return fail(GS_ERR_ARG, "too many work items for the 32-bit work queue");
 
     // This launch's slot.  A slot whose last launch ran on this very stream is reused first:
@@ -2860,7 +2917,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
 
 // Placement pilot.  Before a scene's first launch, when its threaded records do not all
 // fit the LDS mirror: render the launch's camera at 1 spp on a grid of every k-th pixel
-// (k chosen for ~128 k pilot pixels) with the GS_FEAT_VISITS instantiation, which counts
+// (k chosen for ~64 k pilot pixels) with the GS_FEAT_VISITS instantiation, which counts
 // the tests of every node and leaf record, then re-place the records by measured visits
 // per byte (place_records) and upload them again.  The static estimate ranks records by
 // geometry alone and misses where the camera's rays actually go (MI355X C4: its mirror
@@ -2871,7 +2928,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
 static gs_status run_pilot(gs_device_scene* ds, const gs_camera* cam, void* stream) {
     const auto t0 = std::chrono::steady_clock::now();
     const int64_t px = (int64_t)cam->image_width * cam->image_height;
-    const int32_t k = std::max<int32_t>(1, (int32_t)std::sqrt((double)px / 131072.0));
+    const int32_t k = std::max<int32_t>(1, (int32_t)std::sqrt((double)px / 65536.0));
     gs_camera pc = *cam;
     pc.image_width = (cam->image_width + k - 1) / k;
     pc.image_height = (cam->image_height + k - 1) / k;

@@ -218,9 +218,9 @@ int32_t gs_version(void);
  * runs a leaf-test pass (0 acts as 1);
  * sample_chunk = samples per work item when the settings run a single batch
  * (max_samples < batch_size, as every fixed-spp render): -1 auto (16, or batch/64 for
- * big batches; halved while the launch has fewer than ~128 items per GPU lane, down to 1
- * (ABI 7: small frames end without a long tail); at most 64 chunks per pixel and at most
- * 4 GiB of chunk sums), 0 never split a pixel, n > 0 explicit.
+ * big batches: at most 64 chunks per pixel, and at most 4 GiB of chunk sums; ABI 7: the
+ * launch's last tiles in queue order in the finest chunks, batch/64 or 1, so a frame
+ * does not end waiting on a few long items), 0 never split a pixel, n > 0 explicit.
  * Chunks keep every sample's RNG stream; a pixel's chunk sums are added in sample order,
  * so only the association of the f64 colour sum differs from the sequential loop. */
 gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf_batch, int32_t sample_chunk);
