@@ -34,6 +34,7 @@
 #include <chrono>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -245,6 +246,21 @@ __device__ __forceinline__ void load_tnode(const uint8_t* s_nodes, const TNode* 
         const u32x4* q = reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(g) + off);
         a = q[0];
         b = q[1];
+    }
+}
+// The same, for the node steps of a pass: when no active lane's record lies outside the
+// mirror (the common case once the mirror holds the most-tested records) the wave takes
+// a scalar branch straight to the LDS reads, with no exec-mask split and no wait on
+// global loads; otherwise each lane reads its own record's memory.
+template <bool LDS_ONLY>
+__device__ __forceinline__ void load_tnode_w(const uint8_t* s_nodes, const TNode* g, uint32_t off, uint32_t lds_bytes,
+                                             u32x4& a, u32x4& b) {
+    if (LDS_ONLY || __builtin_expect(__builtin_amdgcn_ballot_w64(off >= lds_bytes) == 0, 1)) {
+        lds_u32x4* q = (lds_u32x4*)(uintptr_t)off;
+        a = q[0];
+        b = q[1];
+    } else {
+        load_tnode<false>(s_nodes, g, off, lds_bytes, a, b);
     }
 }
 // 1/d for the f64 slab test on the rare paths.  The asm barrier keeps the compiler from
@@ -1032,6 +1048,9 @@ __host__ __device__ constexpr size_t lane_lds_bytes(bool chunked) {
 }
 
 template <int FEAT>
+#ifdef GS_NUM_VGPR
+__attribute__((amdgpu_num_vgpr(GS_NUM_VGPR)))
+#endif
 __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs A) {
     extern __shared__ __align__(16) uint8_t smem[];
 #ifdef GS_STAMPS
@@ -1415,7 +1434,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #ifndef GS_NODE_STEPS
 #define GS_NODE_STEPS 8
 #endif
-                auto node_step = [&]() __attribute__((always_inline)) {
+                // FAST (compile time): the wave's rays are all cert rays (wave_fast, uniform
+                // for the pass), so the 8 unrolled steps carry no per-step flavour test.
+                auto node_step = [&](auto fast_tag) __attribute__((always_inline)) {
+                constexpr bool FAST = decltype(fast_tag)::value;
 #ifdef GS_STAMPS
                 {
                     const bool glob = !((FEAT & GS_FEAT_LDSTREE) != 0) && cur < THR_END && cur >= (A.lds_nodes << 5);
@@ -1431,16 +1453,16 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     // One 32-B record (2 x 16 B off the SGPR base, offset = cur << 5), the
                     // box test, and the next record: the hit link or the miss link.
                     u32x4 ra, rb;
-                    load_tnode<(FEAT & GS_FEAT_LDSTREE) != 0>(s_nodes, A.tnodes, cur, A.lds_nodes << 5, ra, rb);
+                    load_tnode_w<(FEAT & GS_FEAT_LDSTREE) != 0>(s_nodes, A.tnodes, cur, A.lds_nodes << 5, ra, rb);
                     c_nodes++;
                     if constexpr ((FEAT & GS_FEAT_VISITS) != 0) count_visit(P->visits, cur >> 5);
                     bool h;
-                    if (wave_fast) {
+                    if constexpr (FAST) {
                         bool undecided;
                         h = box_cert(__uint_as_float(ra.x), __uint_as_float(ra.y), __uint_as_float(rb.x),
                                      __uint_as_float(ra.z), __uint_as_float(ra.w), __uint_as_float(rb.y), rc, tmin32,
                                      closest32, undecided);
-                        if (undecided) {  // undecided by f32 (rare): the reference's f64 test
+                        if (__builtin_expect(undecided, 0)) {  // undecided by f32 (rare): the reference's f64 test
                             GS_MARK("fallback_begin");
                             h = box_hit_fast(box64(A.tboxes[cur >> 5]), ray.o, inv_of(ray.d), tmin, closest);
                             GS_MARK("fallback_end");
@@ -1482,12 +1504,18 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 // The scene's step count (gs_device_scene.node_steps): the full count as one
                 // unrolled block (a runtime exit inside it keeps the loop rolled: -1.5% on C4),
                 // fewer steps (trees of other-kind leaves) as a loop.
-                if (A.node_steps >= GS_NODE_STEPS) {
+                // Waves holding a non-cert ray (rare) take the f64 test in a rolled loop.
+                using fast_t = std::integral_constant<bool, true>;
+                using slow_t = std::integral_constant<bool, false>;
+                if (wave_fast && A.node_steps >= GS_NODE_STEPS) {
 #pragma unroll
-                    for (int nstep = 0; nstep < GS_NODE_STEPS; nstep++) node_step();
+                    for (int nstep = 0; nstep < GS_NODE_STEPS; nstep++) node_step(fast_t{});
+                } else if (wave_fast) {
+#pragma unroll 1
+                    for (int nstep = 0; nstep < A.node_steps; nstep++) node_step(fast_t{});
                 } else {
 #pragma unroll 1
-                    for (int nstep = 0; nstep < A.node_steps; nstep++) node_step();
+                    for (int nstep = 0; nstep < A.node_steps; nstep++) node_step(slow_t{});
                 }
                 GS_MARK("node_end");
             } else if (at_leaf) {

@@ -23,8 +23,10 @@ def main():
     ap.add_argument("root")
     ap.add_argument("out")
     ap.add_argument("--kernel", default="gs_render_kernel")
+    ap.add_argument("--exclude", default="gs_render_kernel<55>",
+                    help="dispatches to skip (default: the placement pilot's instantiation, GS_FEAT_PILOT)")
     ap.add_argument("--config", default="C4")
-    ap.add_argument("--round", type=int, default=2)
+    ap.add_argument("--round", type=int, default=3)
     ap.add_argument("--lib", default=None, help="the library profiled (default: the in-tree libgrayshift.so)")
     a = ap.parse_args()
     import sys
@@ -38,7 +40,7 @@ def main():
     dur = []
     for f in sorted(glob.glob(os.path.join(a.root, "pmc_*", "run_counter_collection.csv"))):
         for row in csv.DictReader(open(f)):
-            if a.kernel not in row["Kernel_Name"]:
+            if a.kernel not in row["Kernel_Name"] or (a.exclude and a.exclude in row["Kernel_Name"]):
                 continue
             name = row["Counter_Name"]
             vals[name] += float(row["Counter_Value"])
@@ -46,7 +48,7 @@ def main():
         kt = f.replace("run_counter_collection.csv", "run_kernel_trace.csv")
         if os.path.exists(kt):
             for row in csv.DictReader(open(kt)):
-                if a.kernel in row["Kernel_Name"]:
+                if a.kernel in row["Kernel_Name"] and not (a.exclude and a.exclude in row["Kernel_Name"]):
                     dur.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6)
     if not vals:
         raise SystemExit("no %s rows under %s/pmc_*" % (a.kernel, a.root))
@@ -76,6 +78,8 @@ def main():
             out["valu_active_frac"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * cyc)
         if "SQ_INSTS_SALU" in c:
             out["salu_issue_frac"] = c["SQ_INSTS_SALU"] / (1024 * cyc)
+    if "SQ_LDS_IDX_ACTIVE" in c and "GRBM_GUI_ACTIVE" in c:
+        out["lds_busy_frac"] = c["SQ_LDS_IDX_ACTIVE"] / (256 * c["GRBM_GUI_ACTIVE"] / 8.0)
     os.makedirs(a.out, exist_ok=True)
     path = os.path.join(a.out, "%s_%s.json" % (a.config, h))
     with open(path, "w") as f:
