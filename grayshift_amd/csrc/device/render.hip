@@ -280,7 +280,13 @@ __device__ __forceinline__ void load_tleaf(const uint8_t* s_leaves, const TLeaf*
                                            uint32_t& ref) {
     u32x4 a, b;
     u32x2 d;
-    if (LDS_ONLY || i < lds_l) {
+    // (as load_tnode_w: one scalar branch when every active lane's record is mirrored)
+    if (LDS_ONLY || __builtin_expect(__builtin_amdgcn_ballot_w64(i >= lds_l) == 0, 1)) {
+        const uint8_t* p = s_leaves + i * 48u;
+        a = ((lds_u32x4*)p)[0];
+        b = ((lds_u32x4*)p)[1];
+        d = *(lds_u32x2*)(p + 32);
+    } else if (i < lds_l) {
         const uint8_t* p = s_leaves + i * 48u;
         a = ((lds_u32x4*)p)[0];
         b = ((lds_u32x4*)p)[1];
@@ -1510,6 +1516,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 if (wave_fast && A.node_steps >= GS_NODE_STEPS) {
 #pragma unroll
                     for (int nstep = 0; nstep < GS_NODE_STEPS; nstep++) node_step(fast_t{});
+                } else if (wave_fast && A.node_steps == 1) {  // (trees of other-kind leaves, C3)
+                    node_step(fast_t{});
                 } else if (wave_fast) {
 #pragma unroll 1
                     for (int nstep = 0; nstep < A.node_steps; nstep++) node_step(fast_t{});
@@ -1543,7 +1551,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                 }
 #endif
-                if ((ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {  // a stationary sphere, inline
+                auto sphere_leaf = [&]() __attribute__((always_inline)) {  // a stationary sphere, inline
                     GS_MARK("sphere_begin");
                     c_sph++;
                     double t;
@@ -1554,6 +1562,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         LI(L_HINST) = GS_REF_NONE;
                     }
                     GS_MARK("sphere_end");
+                };
+                if ((ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {
+                    sphere_leaf();
                 } else {
                     GS_MARK("other_begin");
                     // A leaf pass whose other-kind lanes all sit at one leaf (the Cornell box:
