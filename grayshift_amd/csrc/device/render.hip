@@ -73,6 +73,8 @@ using namespace gsd;
                           // media / nested-BVH scenes always stage.  MI355X: C4 +2.2%, C5 +1.6%
                           // staged, C3 (Lambertian + light) -2.8% staged
 #define GS_FEAT_VISITS 32 // count tests per threaded record (the placement pilot, run_pilot)
+#define GS_FEAT_SPHLEAF 64 // every top-level leaf is a stationary sphere (no media / nested BVHs):
+                           // leaf passes without the other kinds' code or the kind test
 // The pilot's instantiation: every code path (any scene), plus the counts.
 #define GS_FEAT_PILOT (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_VISITS)
 
@@ -1563,9 +1565,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                     GS_MARK("sphere_end");
                 };
-                if ((ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {
+                if ((FEAT & GS_FEAT_SPHLEAF) != 0 || (ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {
                     sphere_leaf();
-                } else {
+                } else if constexpr ((FEAT & GS_FEAT_SPHLEAF) == 0) {
                     GS_MARK("other_begin");
                     // A leaf pass whose other-kind lanes all sit at one leaf (the Cornell box:
                     // always, with single node steps) tests it with scalar loads.
@@ -1595,7 +1597,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 for (int k = 1; (FEAT & GS_FEAT_LEAFRUN) && k < GS_LEAF_RUN && cur > THR_END; k++) {
                     load_tleaf<(FEAT & GS_FEAT_LDSTREE) != 0>(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr,
                                                          next, ref);
-                    if ((ref >> GS_REF_SHIFT) != GS_REF_SPHERE) break;
+                    if ((FEAT & GS_FEAT_SPHLEAF) == 0 && (ref >> GS_REF_SHIFT) != GS_REF_SPHERE) break;
                     if constexpr ((FEAT & GS_FEAT_VISITS) != 0)
                         count_visit(P->visits, P->visit_leaf_base + (cur & ~THR_LEAF));
                     c_sph++;
@@ -2320,7 +2322,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ThreadedTree tree_keep;  // kept by the scene: re-placed after a launch's pilot (place_records)
     std::vector<uint32_t> placed_pos;
     double nodes_per_leaf = 0.0, other_leaf_frac = 0.0;
-    bool leaf_runs = false;
+    bool leaf_runs = false, sph_leaves = false;
     int32_t auto_node_steps = GS_NODE_STEPS;
     {
         // Iterative pre-order: a node pushes a "close" marker below its children, which
@@ -2427,6 +2429,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                 pairs += i + 1 < n && is_sph(i) && is_sph(i + 1);
             }
             leaf_runs = leaves && pairs * 4 >= leaves;
+            sph_leaves = leaves > 0;
+            for (uint32_t i = 0; i < n && sph_leaves; i++) sph_leaves = !thr_leaf[i] || is_sph(i);
             // Node steps per node pass (MI355X, Msamples/s).  Sphere-only trees take long
             // node runs (C4: 3 -> 6101, 8 -> 6347).  Trees whose leaf tests are mostly other
             // kinds keep their lanes in step, one node per pass, so that a leaf pass finds
@@ -2595,6 +2599,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         const int cases = (int)lamb + (int)metal + (int)diel + (int)iso + (int)(s->background.kind != GS_BG_SOLID);
         if (cases >= 3 && !(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED))) ds->feat |= GS_FEAT_MIXED;
     }
+    if (sph_leaves && leaf_runs && !(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED))) ds->feat |= GS_FEAT_SPHLEAF;
     ds->cert_boxes = cert_boxes;
     ds->node_steps = auto_node_steps;
     ds->tree = std::move(tree_keep);
@@ -2684,6 +2689,13 @@ static void (*kernel_for(int feat))(KArgs) {
         case GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN:
             return gs_render_kernel<GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN>;
         case GS_FEAT_PILOT: return gs_render_kernel<GS_FEAT_PILOT>;
+        case GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN: return gs_render_kernel<GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN>;
+        case GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_LDSTREE:
+            return gs_render_kernel<GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_LDSTREE>;
+        case GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED:
+            return gs_render_kernel<GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED>;
+        case GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_LDSTREE:
+            return gs_render_kernel<GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_LDSTREE>;
         default: return gs_render_kernel<0>;
     }
 }

@@ -266,6 +266,7 @@ typedef struct gs_scene_info {
     uint32_t node_records, leaf_records;
     uint32_t lds_nodes, lds_leaves, lds_quads;
     int32_t feat;       /* kernel features: 1 media, 2 nested BVHs, 4 sphere leaf runs, 8 whole tree in LDS,
+                           64 every top-level leaf a stationary sphere (ABI 7),
                            16 staged shading (three or more shading cases share its stages) */
     int32_t node_steps; /* node steps per node pass the scene's launches use (see gs_set_node_steps) */
     int32_t cert_boxes; /* every node coordinate |x| <= 1e15: the certified f32 box test applies */
