@@ -1105,8 +1105,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #endif
     // BVHs under instances keep round 1's advance / begin_ray sites (see the shade pass)
     constexpr bool kOldSites = GS_NESTED_SITES && (FEAT & GS_FEAT_NESTED) != 0;
+    // Every top-level leaf a stationary sphere: no instance is ever hit, so the hit's
+    // instance (lane state L_HINST) stays GS_REF_NONE from the kernel's start.
+    constexpr bool kSphLeaf = (FEAT & GS_FEAT_SPHLEAF) != 0;
 #define LD(k) s_d[(k) * GS_BLOCK + tid]
 #define LI(k) s_i[(k) * GS_BLOCK + tid]
+    if constexpr (kSphLeaf) LI(L_HINST) = GS_REF_NONE;
 
     uint32_t st = S_NEED;
     bool qdone = false;
@@ -1141,7 +1145,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         closest = 1.7976931348623157e308;  // f64::MAX (camera.rs:177)
         closest32 = __builtin_inff();
         hit_ref = GS_REF_NONE;
-        LI(L_HINST) = GS_REF_NONE;
+        if constexpr (!kSphLeaf) LI(L_HINST) = GS_REF_NONE;  // (sphere-only trees: never set)
         atomicAdd(&s_cnt[C_RAYS], 1ull);
     };
 
@@ -1561,7 +1565,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         closest = t;
                         closest32 = (float)t;
                         hit_ref = ref;
-                        LI(L_HINST) = GS_REF_NONE;
+                        if constexpr (!kSphLeaf) LI(L_HINST) = GS_REF_NONE;
                     }
                     GS_MARK("sphere_end");
                 };
@@ -1606,7 +1610,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         closest = t;
                         closest32 = (float)t;
                         hit_ref = ref;
-                        LI(L_HINST) = GS_REF_NONE;
+                        if constexpr (!kSphLeaf) LI(L_HINST) = GS_REF_NONE;
                     }
                     cur = next;
                 }
@@ -1999,11 +2003,16 @@ static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* 
         (t.leaf[r] ? out.lds_leaves : out.lds_nodes)++;
     }
     out.lds_quads = (uint32_t)std::min<int64_t>(n_quads, std::max<int64_t>(0, budget - used) / (int64_t)sizeof(TQuad));
+    // The mirrored records take their positions in rank order, so a launch that must
+    // shrink the prefixes (a larger lane state, gs_render_tiles_timed_async) drops the
+    // least-tested ones; the rest keep pre-order.
     uint32_t nt = 0, nl = 0, nt_rest = out.lds_nodes, nl_rest = out.lds_leaves;
-    for (uint32_t i = 0; i < n; i++) {
-        if (t.leaf[i]) pos[i] = top[i] ? nl++ : nl_rest++;
-        else pos[i] = top[i] ? nt++ : nt_rest++;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t i = order[k];
+        if (top[i]) pos[i] = t.leaf[i] ? nl++ : nt++;
     }
+    for (uint32_t i = 0; i < n; i++)
+        if (!top[i]) pos[i] = t.leaf[i] ? nl_rest++ : nt_rest++;
     out.tnodes.resize(nt_rest);
     out.tboxes.resize(nt_rest);
     out.tleaves.resize(nl_rest);
