@@ -258,6 +258,37 @@ __device__ __forceinline__ bool sphere_accept(d3 c, double r, const Ray& ray, do
     return true;
 }
 
+// sphere_accept split in two (the same operations in the same order): the roots, which
+// do not depend on the ray interval, and the acceptance against it.  Lets a leaf pass
+// compute two spheres' roots as independent chains before accepting them in order.
+struct SphereRoots {
+    double t1, t2;  // (h - sqrt(disc)) / a, (h + sqrt(disc)) / a
+    bool real;      // disc >= 0
+};
+__device__ __forceinline__ SphereRoots sphere_roots(d3 c, double r, const Ray& ray, double a) {
+    d3 oc = sub(c, ray.o);
+    double h = dot(ray.d, oc);
+    double cc = len2(oc) - r * r;
+    double disc = h * h - a * cc;
+    SphereRoots s;
+    s.real = !(disc < 0.0);
+    double sq = sqrt(s.real ? disc : 0.0);
+    s.t1 = (h - sq) / a;
+    s.t2 = (h + sq) / a;
+    return s;
+}
+__device__ __forceinline__ bool sphere_take(const SphereRoots& s, double tmin, double tmax, double& t_out) {
+    t_out = tmax;
+    if (!s.real) return false;
+    double t = s.t1;
+    if (!(tmin < t && t < tmax)) {
+        t = s.t2;
+        if (!(tmin < t && t < tmax)) return false;
+    }
+    t_out = t;
+    return true;
+}
+
 // HDRI::sample's texel column and row (camera.rs:257-270) for the rotated, normalised
 // direction `rot`: u = 0.5 + atan2(y, x) / 2pi, v = 0.5 - asin(z) / pi, then
 // `(u * W) as usize % W`, `(v * H) as usize % H`.  sky_index_f64 is that, in f64.

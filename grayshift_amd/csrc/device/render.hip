@@ -401,6 +401,8 @@ __device__ __forceinline__ bool quad_test(const QuadSrc& qs, uint32_t i, const R
         ray, tmin, tmax, t_out);
 }
 
+__device__ __forceinline__ bool cur_next_is_leaf(uint32_t link) { return link > THR_END; }
+
 // Outcome of testing one non-node child against the ray.
 struct LeafHit {
     bool hit;
@@ -1569,7 +1571,41 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                     GS_MARK("sphere_end");
                 };
-                if ((FEAT & GS_FEAT_SPHLEAF) != 0 || (ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {
+#ifndef GS_LEAF_ILP
+#define GS_LEAF_ILP 1
+#endif
+                if constexpr ((FEAT & GS_FEAT_SPHLEAF) != 0 && GS_LEAF_ILP) {
+                    // Sphere-only trees: a leaf run's second sphere (the next record, when it
+                    // is a leaf) is read right away and both spheres' roots are computed as
+                    // two independent chains; they are then accepted in order, the second
+                    // against the interval the first left (sphere.rs:64-89, BVH.rs:73-80).
+                    const bool two = cur_next_is_leaf(next);
+                    double s2x, s2y, s2z, s2r;
+                    uint32_t next2, ref2;
+                    load_tleaf<(FEAT & GS_FEAT_LDSTREE) != 0>(s_leaves, A.tleaves, two ? next & ~THR_LEAF : cur & ~THR_LEAF,
+                                                             A.lds_leaves, s2x, s2y, s2z, s2r, next2, ref2);
+                    const double a = len2(ray.d);
+                    const SphereRoots q1 = sphere_roots(mk(scx, scy, scz), sr, ray, a);
+                    const SphereRoots q2 = sphere_roots(mk(s2x, s2y, s2z), s2r, ray, a);
+                    GS_MARK("sphere_begin");
+                    double t;
+                    if (sphere_take(q1, tmin, closest, t)) {
+                        closest = t;
+                        hit_ref = ref;
+                    }
+                    if (two) {
+                        if constexpr ((FEAT & GS_FEAT_VISITS) != 0)
+                            count_visit(P->visits, P->visit_leaf_base + (next & ~THR_LEAF));
+                        if (sphere_take(q2, tmin, closest, t)) {
+                            closest = t;
+                            hit_ref = ref2;
+                        }
+                        next = next2;
+                    }
+                    closest32 = (float)closest;
+                    c_sph += 1u + (uint32_t)two;
+                    GS_MARK("sphere_end");
+                } else if ((FEAT & GS_FEAT_SPHLEAF) != 0 || (ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {
                     sphere_leaf();
                 } else if constexpr ((FEAT & GS_FEAT_SPHLEAF) == 0) {
                     GS_MARK("other_begin");
@@ -1598,7 +1634,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 // A template feature: trees without such pairs (the Cornell box's quads and
                 // instances) lose ~2% to the loop's mere presence (MI355X C3).
 #pragma unroll 1
-                for (int k = 1; (FEAT & GS_FEAT_LEAFRUN) && k < GS_LEAF_RUN && cur > THR_END; k++) {
+                for (int k = 1; (FEAT & GS_FEAT_LEAFRUN) && !((FEAT & GS_FEAT_SPHLEAF) != 0 && GS_LEAF_ILP) &&
+                                k < GS_LEAF_RUN && cur > THR_END; k++) {
                     load_tleaf<(FEAT & GS_FEAT_LDSTREE) != 0>(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr,
                                                          next, ref);
                     if ((FEAT & GS_FEAT_SPHLEAF) == 0 && (ref >> GS_REF_SHIFT) != GS_REF_SPHERE) break;
