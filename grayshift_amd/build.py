@@ -37,6 +37,7 @@ DEPS = SOURCES + [
     os.path.join(ROOT, "include", "grayshift_gpu.h"),
     os.path.join(ROOT, "include", "grayshift_host.h"),
     os.path.join(ROOT, "include", "grayshift_scene.h"),
+    os.path.abspath(__file__),  # the compiler flags
 ]
 
 ARCH = os.environ.get("GS_OFFLOAD_ARCH", "gfx950")
@@ -69,6 +70,11 @@ def build_product(force=False, verbose=False, extra=(), out=None):
             # and reloads each one with a dependent scratch load: measured on MI355X C4,
             # disabling it removes all scratch and runs +19% (1990 -> 2370 Msamples/s).
             cmd += ["-x", "hip", "--offload-arch=" + ARCH, "-mllvm", "-disable-machine-licm"]
+            # A fixed compilation-unit id: clang's default hashes the command line, -o
+            # included, into a symbol of the code object, so the same sources built into
+            # another directory would hash differently (grayshift_amd/codeobj.py keys the
+            # committed PMC summaries by the code objects' hash).
+            cmd += ["-cuid=gs_" + os.path.basename(src).replace(".", "_")]
         cmd += ["-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)

@@ -162,6 +162,15 @@ __device__ __forceinline__ bool box_hit_fast(const DNode& n, const d3& o, const 
 //         covering the rounding of d and thr themselves),
 // d = hi' - lo' > thr certifies the f64 hit (hi > lo) and d < -thr its miss (hi <= lo);
 // the 1e-30 covers f32 underflow.  All values stay finite (|t'| < 2e30), so no NaN.
+//
+// The kernel drops both absolute values (round 3: two VOP3 source modifiers fewer per node
+// step), thr' = K (hi' + lo') + 2 K R + 1e-30:  lo' >= tmin' = f32(0.001) > 0, so |lo'| =
+// lo'; and hi' replaces |hi'|.  For hi' >= 0 nothing changes.  For hi' < 0, (a) d > thr'
+// would need hi' (1 - K) > lo' (1 + K) + ... > 0, so no hit is certified, as with thr; (b)
+// a miss is certified when d < -thr', i.e. lo' (1 - K) + |hi'| (1 + K) > 2 K R + 1e-30, so
+// lo' + |hi'| > 16 u R / (1 + 8u), and the exact miss needs only lo' - hi' = lo' + |hi'| >
+// 3.01u (|hi'| + lo' + 2R): (1 - 3.01u)(lo' + |hi'|) > 15.8 u R > 6.02 u R.  Undecided is
+// then -thr' <= d <= thr'.
 #define GS_CERT_K 4.76837158203125e-07f  // 2^-21
 
 struct alignas(16) TNode {  // 32 B record of the threaded tree: f32 box (paired for box_cert) + hit / miss links
@@ -209,9 +218,10 @@ __device__ __forceinline__ RayCert make_cert(const d3& o, const d3& inv) {
     c.r2 = (float)(2.0 * (double)GS_CERT_K * R * (1.0 + 0x1p-20)) + 1e-30f;
     return c;
 }
-// Returns the certified decision (hit); `undecided` when f32 cannot decide (run the f64 test).
-__device__ __forceinline__ bool box_cert(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
-                                         const RayCert& c, float tmin32, float closest32, bool& undecided) {
+// The certified test's difference and threshold: returns d > thr (a certified hit);
+// d < -thr is a certified miss, anything between undecided (run the f64 test).
+__device__ __forceinline__ bool box_cert_dt(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                            const RayCert& c, float tmin32, float closest32, float& d, float& thr) {
     // t = fma(coordinate, 1/d, -o/d) for both planes of an axis at once
     const gs_f2 t0 = __builtin_elementwise_fma(gs_f2{mnx, mny}, c.ixy, c.oxy);
     const gs_f2 t1 = __builtin_elementwise_fma(gs_f2{mxx, mxy}, c.ixy, c.oxy);
@@ -221,10 +231,17 @@ __device__ __forceinline__ bool box_cert(float mnx, float mny, float mnz, float 
                                      __builtin_fmaxf(__builtin_fminf(t0y, t1y), __builtin_fminf(t0z, t1z)));
     const float hi = __builtin_fminf(__builtin_fminf(closest32, __builtin_fmaxf(t0x, t1x)),
                                      __builtin_fminf(__builtin_fmaxf(t0y, t1y), __builtin_fmaxf(t0z, t1z)));
-    const float d = hi - lo;
-    const float thr = __builtin_fmaf(GS_CERT_K, __builtin_fabsf(hi) + __builtin_fabsf(lo), c.r2);
-    undecided = __builtin_fabsf(d) <= thr;
+    d = hi - lo;
+    thr = __builtin_fmaf(GS_CERT_K, hi + lo, c.r2);  // lo >= tmin32 > 0; hi for |hi| (above)
     return d > thr;
+}
+// Returns the certified decision (hit); `undecided` when f32 cannot decide (run the f64 test).
+__device__ __forceinline__ bool box_cert(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                         const RayCert& c, float tmin32, float closest32, bool& undecided) {
+    float d, thr;
+    const bool h = box_cert_dt(mnx, mny, mnz, mxx, mxy, mxz, c, tmin32, closest32, d, thr);
+    undecided = !h && d >= -thr;
+    return h;
 }
 __device__ __forceinline__ DNode box64(const TBox& b) {
     DNode n;

@@ -113,7 +113,9 @@ struct alignas(16) DMaterial {
 enum { C_RAYS = 0, C_NODES, C_SPH, C_MSPH, C_QUAD, C_TRI, C_INST, C_LIST, C_HITS, C_IMG, C_HDRI, C_PATHS, C_PIX, C_MED, C_NOISE, C_N };
 
 struct DevScene {
-    const DNode* nodes;
+    const DNode* nodes;   // nested trees' records with their f64 boxes (the f64 test)
+    const TNode* nrecs;   // the same records for the certified f32 test (nested_bvh)
+    uint32_t nested_cert; // every nested node coordinate |x| <= 1e15 (box_cert applies)
     const DSphere* spheres;
     const uint32_t* sphere_mat;
     const gs_msphere* mspheres;
@@ -491,7 +493,11 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
                                             double closest, uint32_t inst_ref, uint64_t& rng, LeafHit& res,
                                             unsigned long long* cnt) {
     atomicAdd(&cnt[C_MED], 1ull);
-    const gs_medium md = ld_medium<UNI>(sc.media + (cur & GS_REF_MASK));
+    // the boundary now, the density only where it is used (not held through both hits)
+    const gs_medium* mp = sc.media + (cur & GS_REF_MASK);
+    struct {
+        uint32_t boundary;
+    } md{ld_u32<UNI>(&mp->boundary)};
     const double DMAX = 1.7976931348623157e308;  // f64::MAX; f64::MIN = -f64::MAX
     LeafHit b1;
     b1.hit = false;
@@ -514,7 +520,7 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
     if (t1 < 0.0) t1 = 0.0;
     const double ray_len = sqrt(len2(r.d));
     const double dist_inside_boundary = (t2 - t1) * ray_len;
-    const double hit_dist = md.density_neg_inv * log(wy_f64(rng));
+    const double hit_dist = sp<UNI>(mp)->density_neg_inv * log(wy_f64(rng));
     if (hit_dist > dist_inside_boundary) return;
     res.hit = true;
     res.t = t1 + hit_dist / ray_len;
@@ -526,26 +532,46 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
 // 741-755): BVHNode::hit (BVH.rs:69-90) on the ray in the instance's space, as the same
 // left-first walk with a shrinking closest t as the top level.  Like the top level, the
 // nested tree is threaded on the host: its pre-order records (one per node, one per leaf
-// occurrence; DNode with pad0 = 1 for a leaf) with a hit / next link (`left`) and a miss
-// link (`right`; a leaf's `right` is its ABI ref), so the walk is `cur = hit ? left :
-// right` with no stack (round 2's private stack cost these instantiations 216 B/lane of
-// scratch).  `root`: the tree's first record.  Leaves are lists or primitives (validated).
+// occurrence) with a hit / next link and a miss link, so the walk is `cur = hit ? hit_link
+// : miss_link` with no stack (round 2's private stack cost these instantiations 216 B/lane
+// of scratch).  And like the top level, a node is decided by the certified f32 test on a
+// 32-B record (TNode: f32 box, hit link, miss link; a leaf: NREC_LEAF | next, ABI ref),
+// with the reference's f64 test (DNode) only where f32 cannot decide or the ray is not a
+// cert ray (round 3: half the bytes per node and fewer registers than the f64 walk).
+// `root`: the tree's first record.  Leaves are lists or primitives (validated).
+#define NREC_LEAF 0x80000000u
 __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs, uint32_t root, const Ray& r, double tmin,
                                            double closest, uint32_t inst_ref, LeafHit& res,
                                            unsigned long long* cnt) {
-    // AABB::hit's `1.0 / ray.direction[axis]` (AABB.rs:64), hoisted per ray (same value)
-    const d3 inv = mk(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
+    bool fast;
+    RayCert c;
+    {
+        // AABB::hit's `1.0 / ray.direction[axis]` (AABB.rs:64), once per walk (same value)
+        const d3 inv = mk(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
+        fast = sc.nested_cert && cert_ray_ok(r.o, inv);
+        c = make_cert(r.o, inv);
+    }
+    float closest32 = (float)closest;
     uint32_t cur = root;
 #pragma unroll 1
     while (cur != THR_END) {
-        const DNode n = ld_node_g(sc.nodes + cur);
-        if (n.pad0) {  // a leaf occurrence: test it, then the next record
-            shape_test<false>(sc, qs, n.right, r, tmin, closest, inst_ref, res, cnt);
-            if (res.hit) closest = res.t;  // res.t only ever shrinks
-            cur = n.left;
+        const u32x4* q = sp<false>(reinterpret_cast<const u32x4*>(sc.nrecs + cur));
+        const u32x4 a = q[0], b = q[1];
+        if (b.z & NREC_LEAF) {  // a leaf occurrence: test it, then the next record
+            shape_test<false>(sc, qs, b.w, r, tmin, closest, inst_ref, res, cnt);
+            if (res.hit) {  // res.t only ever shrinks
+                closest = res.t;
+                closest32 = (float)res.t;
+            }
+            cur = b.z & ~NREC_LEAF;
         } else {
             atomicAdd(&cnt[C_NODES], 1ull);
-            cur = box_hit_v(n, r.o, inv, tmin, closest) ? n.left : n.right;
+            bool h = false, undecided = true;
+            if (fast)
+                h = box_cert(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(b.x), __uint_as_float(a.z),
+                             __uint_as_float(a.w), __uint_as_float(b.y), c, 0.001f, closest32, undecided);
+            if (undecided) h = box_hit_v(ld_node_g(sc.nodes + cur), r.o, inv_of(r.d), tmin, closest);
+            cur = h ? b.z : b.w;
         }
     }
 }
@@ -1001,7 +1027,6 @@ __device__ GS_NOINLINE Scatter scatter(const DevScene& sc, HitRec h, d3 in_dir, 
     return s;
 }
 
-__device__ __forceinline__ uint64_t lanemask_lt(uint32_t lane) { return (1ull << lane) - 1ull; }
 
 // The placement pilot's count (GS_FEAT_VISITS): one atomic per distinct record among the
 // wave's active lanes (every ray of a pilot tests the root and the records below it: one
@@ -1052,9 +1077,25 @@ enum { L_ITEM = 0, L_PIX, L_BLEFT, L_SAMPLE, L_DEPTH, L_HINST, L_NI };  // (samp
 // Fixed-spp (chunked) launches never reach the stop test, so their lanes keep only the
 // three colour sums: the 24 KiB of Σlum / Σlum² / sample-count slots go to the mirror.
 enum { L_ND_CHUNKED = L_LSUM };
-__host__ __device__ constexpr uint32_t lane_nd(bool chunked) { return chunked ? (uint32_t)L_ND_CHUNKED : (uint32_t)L_ND; }
-__host__ __device__ constexpr size_t lane_lds_bytes(bool chunked) {
-    return (size_t)GS_BLOCK * (lane_nd(chunked) * 8 + L_NI * 4) + 128 + GS_STAMP_LDS;
+// Media / nested-BVH kernels keep the path throughput (Tr, Tg, Tb: read and written only
+// by the shade pass) in three more f64 lane fields (before those), out of the registers their
+// leaf tests need (round 3: with them in VGPRs these instantiations spilled 52-76 B/lane).
+#ifndef GS_T_LDS
+#define GS_T_LDS 1
+#endif
+// (not the placement pilot's counting kernel: it launches with the scene's own lane layout)
+__host__ __device__ constexpr bool t_in_lds(int feat) {
+    return GS_T_LDS && (feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED)) != 0 && (feat & GS_FEAT_VISITS) == 0;
+}
+__host__ __device__ constexpr uint32_t lane_nd(bool chunked, int feat) {
+    return (chunked ? (uint32_t)L_ND_CHUNKED : (uint32_t)L_ND) + (t_in_lds(feat) ? 3u : 0u);
+}
+// ... and the hit primitive's ref (written by leaf tests, read by the shade pass) in one
+// more u32 field, L_HREF.
+enum { L_HREF = L_NI };
+__host__ __device__ constexpr uint32_t lane_ni(int feat) { return (uint32_t)L_NI + (t_in_lds(feat) ? 1u : 0u); }
+__host__ __device__ constexpr size_t lane_lds_bytes(bool chunked, int feat) {
+    return (size_t)GS_BLOCK * (lane_nd(chunked, feat) * 8 + lane_ni(feat) * 4) + 128 + GS_STAMP_LDS;
 }
 
 template <int FEAT>
@@ -1088,7 +1129,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     // Per-lane pixel / path state after the mirror: [L_ND][GS_BLOCK] f64, [L_NI][GS_BLOCK] u32.
     double* s_d = (double*)(s_quads + (size_t)A.lds_quads * sizeof(TQuad));
     uint32_t* s_i = (uint32_t*)(s_d + A.lane_nd * GS_BLOCK);
-    unsigned long long* s_cnt = (unsigned long long*)(s_i + L_NI * GS_BLOCK);
+    unsigned long long* s_cnt = (unsigned long long*)(s_i + lane_ni(FEAT) * GS_BLOCK);
 #ifdef GS_STAMPS
     unsigned long long* s_reg = s_cnt + 16;  // [(GS_BLOCK / 64) * 8]
     if (threadIdx.x < (GS_BLOCK / 64) * 8) s_reg[threadIdx.x] = 0;
@@ -1101,6 +1142,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     const gs_camera& cam = P->cam;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t tid = threadIdx.x;
+    const uint64_t flushers = __builtin_amdgcn_ballot_w64(tid < C_N);  // the counters' flushing lanes
     const double tmin = 0.001;
 #ifndef GS_NESTED_SITES
 #define GS_NESTED_SITES 1
@@ -1110,7 +1152,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     // Every top-level leaf a stationary sphere: no instance is ever hit, so the hit's
     // instance (lane state L_HINST) stays GS_REF_NONE from the kernel's start.
     constexpr bool kSphLeaf = (FEAT & GS_FEAT_SPHLEAF) != 0;
-#define LD(k) s_d[(k) * GS_BLOCK + tid]
+    // (t_in_lds kernels: the throughput's three fields first, at fixed offsets)
+#define LD(k) s_d[((k) + (t_in_lds(FEAT) ? 3 : 0)) * GS_BLOCK + tid]
 #define LI(k) s_i[(k) * GS_BLOCK + tid]
     if constexpr (kSphLeaf) LI(L_HINST) = GS_REF_NONE;
 
@@ -1119,14 +1162,22 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     uint32_t res_base = 0, res_cnt = 0;  // the wave's reserve of claimed items (wave-uniform)
     // path state (registers)
     uint64_t rng = 0;
-    double Tr = 1, Tg = 1, Tb = 1;
+    // path throughput: registers, or the last three f64 lane fields (t_in_lds)
+    constexpr bool kTLds = t_in_lds(FEAT);
+    double Tr_ = 1, Tg_ = 1, Tb_ = 1;
+#define GS_TP(reg, k) (*(kTLds ? &s_d[(k) * GS_BLOCK + tid] : &(reg)))
+#define Tr GS_TP(Tr_, 0)
+#define Tg GS_TP(Tg_, 1)
+#define Tb GS_TP(Tb_, 2)
     Ray ray;
     ray.o = mk(0, 0, 0);
     ray.d = mk(0, 0, 0);
     ray.time = 0;
     RayCert rc{};  // the ray in the certified f32 slab test's terms (geometry.hpp)
     // traversal state
-    uint32_t cur = THR_END, hit_ref = GS_REF_NONE;
+    uint32_t cur = THR_END, hit_ref_ = GS_REF_NONE;
+    // the hit primitive's ref: a register, or the lane's L_HREF field (t_in_lds kernels)
+    uint32_t& hit_ref = kTLds ? s_i[L_HREF * GS_BLOCK + tid] : hit_ref_;
     double closest = 0.0;
     float closest32 = 0.0f;  // f32(closest)
     const float tmin32 = 0.001f;  // f32(tmin)
@@ -1168,6 +1219,22 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     // Start samples until one needs tracing or the pixel is finished:
     // leaves st = S_TRACE (ray ready) or S_NEED (pixel written).
     // End of a chunk: its Σrgb, summed per pixel by gs_combine_kernel.
+    // The lane's node-visit and sphere-test counts go to the block's counters at the end of
+    // the kernel -- or at an item's end when the launch records per-item visits (the tile
+    // plan's pilot), or before a count could overflow.  (Flushing at every item's end ran
+    // the compiler's lane-serial reduction loop of two 64-bit atomics per chunk.)
+    auto flush_counts = [&]() {
+        atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
+        atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
+        c_nodes = 0;
+        c_sph = 0;
+    };
+    // a stationary-sphere test: a lane count (flushed with c_nodes), or in t_in_lds kernels
+    // a wave-aggregated LDS atomic, as prim_test counts the other kinds (no register kept)
+    auto count_sph = [&]() __attribute__((always_inline)) {
+        if constexpr (kTLds) atomicAdd(&s_cnt[C_SPH], 1ull);
+        else c_sph++;
+    };
     auto end_chunk = [&]() {
         const uint32_t item = LI(L_ITEM);
         double* o = P->partial + (size_t)item * 3;
@@ -1175,12 +1242,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         o[1] = LD(L_CSG);
         o[2] = LD(L_CSB);
 #if !defined(GS_STAMPS) && !defined(GS_CERT_CHECK)  // (those builds use item_visits as their record buffer)
-        if (P->item_visits) atomicAdd(&P->item_visits[item / P->cpp], c_nodes);
+        if (P->item_visits) {
+            atomicAdd(&P->item_visits[item / P->cpp], c_nodes);
+            flush_counts();
+        }
 #endif
-        atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
-        atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
-        c_nodes = 0;
-        c_sph = 0;
+        if ((c_nodes | c_sph) >= (1u << 30)) flush_counts();
         st = S_NEED;
     };
 
@@ -1218,12 +1285,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                     atomicAdd(&s_cnt[C_PIX], 1ull);
 #if !defined(GS_STAMPS) && !defined(GS_CERT_CHECK)
-                    if (P->item_visits) P->item_visits[item] = c_nodes;
+                    if (P->item_visits) {
+                        P->item_visits[item] = c_nodes;
+                        flush_counts();
+                    }
 #endif
-                    atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
-                    atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
-                    c_nodes = 0;
-                    c_sph = 0;
+                    if ((c_nodes | c_sph) >= (1u << 30)) flush_counts();
                     st = S_NEED;
                     return;
                 }
@@ -1313,7 +1380,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             res_cnt -= take;
             const uint32_t tile_px = (uint32_t)(P->tile_w * P->tile_h);
             const bool blocked8 = (P->tile_w % 8 == 0) && (P->tile_h % 8 == 0);
-            const uint32_t rank = (uint32_t)__popcll(need & lanemask_lt(lane));
+            // set bits of `need` below this lane (v_mbcnt: no 64-bit lane mask kept live)
+            const uint32_t rank =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
             if (st == S_NEED && rank < take) {
                 const uint64_t q = (uint64_t)base + (uint64_t)rank;
                 if (q >= P->n_items) {
@@ -1450,35 +1519,52 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #endif
                 // FAST (compile time): the wave's rays are all cert rays (wave_fast, uniform
                 // for the pass), so the 8 unrolled steps carry no per-step flavour test.
-                auto node_step = [&](auto fast_tag) __attribute__((always_inline)) {
+                // LDSP (compile time): no node lane of the wave sits at a record outside the
+                // LDS mirror when the pass starts (always with the whole tree mirrored), so a
+                // step's one compare, cur < lim, picks the lanes that step -- and reads LDS; a
+                // lane whose walk leaves the mirror parks there until the next pass, which
+                // then runs the mixed flavour (each step splitting its lanes by memory).
+                const uint32_t lim = (FEAT & GS_FEAT_LDSTREE) != 0 ? (uint32_t)THR_END : A.lds_nodes << 5;
+                auto node_step = [&](auto fast_tag, auto ldsp_tag) __attribute__((always_inline)) {
                 constexpr bool FAST = decltype(fast_tag)::value;
+                constexpr bool LDSP = decltype(ldsp_tag)::value;
 #ifdef GS_STAMPS
                 {
                     const bool glob = !((FEAT & GS_FEAT_LDSTREE) != 0) && cur < THR_END && cur >= (A.lds_nodes << 5);
-                    const uint64_t act = __builtin_amdgcn_ballot_w64(cur < THR_END);
-                    const uint64_t gl = __builtin_amdgcn_ballot_w64(glob);
-                    d_gvis += glob;
+                    const uint64_t act = __builtin_amdgcn_ballot_w64(LDSP ? cur < lim : cur < THR_END);
+                    const uint64_t gl = __builtin_amdgcn_ballot_w64(glob && !LDSP);
+                    d_gvis += glob && !LDSP;
                     d_wsteps += act != 0;
                     d_wsteps_g += gl != 0;
                     d_wlanes += (uint64_t)__popcll(act);
                 }
 #endif
-                if (cur < THR_END) {
-                    // One 32-B record (2 x 16 B off the SGPR base, offset = cur << 5), the
-                    // box test, and the next record: the hit link or the miss link.
+                if (__builtin_expect(LDSP ? cur < lim : cur < THR_END, 1)) {
+                    // One 32-B record (2 x 16 B; from LDS, offset = cur, or off the SGPR
+                    // base), the box test, and the next record: the hit link or the miss link.
                     u32x4 ra, rb;
-                    load_tnode_w<(FEAT & GS_FEAT_LDSTREE) != 0>(s_nodes, A.tnodes, cur, A.lds_nodes << 5, ra, rb);
+                    if constexpr (LDSP) {
+                        lds_u32x4* q = (lds_u32x4*)(uintptr_t)cur;
+                        ra = q[0];
+                        rb = q[1];
+                    } else {
+                        load_tnode_w<(FEAT & GS_FEAT_LDSTREE) != 0>(s_nodes, A.tnodes, cur, A.lds_nodes << 5, ra, rb);
+                    }
                     c_nodes++;
                     if constexpr ((FEAT & GS_FEAT_VISITS) != 0) count_visit(P->visits, cur >> 5);
-                    bool h;
+                    const uint32_t me = cur;  // this record
                     if constexpr (FAST) {
-                        bool undecided;
-                        h = box_cert(__uint_as_float(ra.x), __uint_as_float(ra.y), __uint_as_float(rb.x),
-                                     __uint_as_float(ra.z), __uint_as_float(ra.w), __uint_as_float(rb.y), rc, tmin32,
-                                     closest32, undecided);
-                        if (__builtin_expect(undecided, 0)) {  // undecided by f32 (rare): the reference's f64 test
+                        // the certified decision picks the link at once; lanes f32 cannot
+                        // decide (rare) run the reference's f64 test out of line
+                        float d, thr;
+                        bool h = box_cert_dt(__uint_as_float(ra.x), __uint_as_float(ra.y), __uint_as_float(rb.x),
+                                             __uint_as_float(ra.z), __uint_as_float(ra.w), __uint_as_float(rb.y), rc,
+                                             tmin32, closest32, d, thr);
+                        cur = h ? rb.z : rb.w;
+                        if (__builtin_expect(__builtin_fabsf(d) <= thr, 0)) {  // undecided by f32: the f64 test
                             GS_MARK("fallback_begin");
-                            h = box_hit_fast(box64(A.tboxes[cur >> 5]), ray.o, inv_of(ray.d), tmin, closest);
+                            h = box_hit_fast(box64(A.tboxes[me >> 5]), ray.o, inv_of(ray.d), tmin, closest);
+                            cur = h ? rb.z : rb.w;
                             GS_MARK("fallback_end");
                         }
 #ifdef GS_CERT_CHECK
@@ -1486,7 +1572,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         // mismatch is counted (counters[15]) and its first 64 cases recorded
                         // (item_visits as f64[64][16]: o, d, f64 box, tmin, closest, f32 verdict).
                         {
-                            const TBox bx = A.tboxes[cur >> 5];
+                            const TBox bx = A.tboxes[me >> 5];
                             const bool h64 = box_hit(box64(bx), ray.o, inv_of(ray.d), tmin, closest);
                             if (h64 != h) {
                                 const unsigned long long k = atomicAdd(&P->counters[15], 1ull);
@@ -1502,10 +1588,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #endif
                     } else {  // a wave with a non-cert ray: the f64 compare-select test
                         GS_MARK("slow_begin");
-                        h = box_hit(box64(A.tboxes[cur >> 5]), ray.o, inv_of(ray.d), tmin, closest);
+                        const bool h = box_hit(box64(A.tboxes[me >> 5]), ray.o, inv_of(ray.d), tmin, closest);
+                        cur = h ? rb.z : rb.w;
                         GS_MARK("slow_end");
                     }
-                    cur = h ? rb.z : rb.w;
 #ifdef GS_PAD_NODE  // calibration builds: GS_PAD_NODE extra f32 VALU ops per node step
                     {
                         float pad = __uint_as_float(ra.x);
@@ -1517,21 +1603,29 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 };
                 // The scene's step count (gs_device_scene.node_steps): the full count as one
                 // unrolled block (a runtime exit inside it keeps the loop rolled: -1.5% on C4),
-                // fewer steps (trees of other-kind leaves) as a loop.
-                // Waves holding a non-cert ray (rare) take the f64 test in a rolled loop.
+                // fewer steps (trees of other-kind leaves) as a loop.  The mixed-memory flavour
+                // (a node lane outside the mirror at the pass start: ~10% of C4's passes) and
+                // waves holding a non-cert ray (rare) take rolled loops.
                 using fast_t = std::integral_constant<bool, true>;
                 using slow_t = std::integral_constant<bool, false>;
-                if (wave_fast && A.node_steps >= GS_NODE_STEPS) {
+                using ldsp_t = std::integral_constant<bool, true>;
+                using mixed_t = std::integral_constant<bool, false>;
+                const bool lds_pass = (FEAT & GS_FEAT_LDSTREE) != 0 ||
+                                      __builtin_amdgcn_ballot_w64(cur < THR_END && cur >= lim) == 0;
+                if (wave_fast && lds_pass && A.node_steps >= GS_NODE_STEPS) {
 #pragma unroll
-                    for (int nstep = 0; nstep < GS_NODE_STEPS; nstep++) node_step(fast_t{});
-                } else if (wave_fast && A.node_steps == 1) {  // (trees of other-kind leaves, C3)
-                    node_step(fast_t{});
+                    for (int nstep = 0; nstep < GS_NODE_STEPS; nstep++) node_step(fast_t{}, ldsp_t{});
+                } else if (wave_fast && lds_pass && A.node_steps == 1) {  // (trees of other-kind leaves, C3)
+                    node_step(fast_t{}, ldsp_t{});
+                } else if (wave_fast && lds_pass) {
+#pragma unroll 1
+                    for (int nstep = 0; nstep < A.node_steps; nstep++) node_step(fast_t{}, ldsp_t{});
                 } else if (wave_fast) {
 #pragma unroll 1
-                    for (int nstep = 0; nstep < A.node_steps; nstep++) node_step(fast_t{});
+                    for (int nstep = 0; nstep < A.node_steps; nstep++) node_step(fast_t{}, mixed_t{});
                 } else {
 #pragma unroll 1
-                    for (int nstep = 0; nstep < A.node_steps; nstep++) node_step(slow_t{});
+                    for (int nstep = 0; nstep < A.node_steps; nstep++) node_step(slow_t{}, mixed_t{});
                 }
                 GS_MARK("node_end");
             } else if (at_leaf) {
@@ -1561,7 +1655,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #endif
                 auto sphere_leaf = [&]() __attribute__((always_inline)) {  // a stationary sphere, inline
                     GS_MARK("sphere_begin");
-                    c_sph++;
+                    count_sph();
                     double t;
                     if (sphere_accept(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
                         closest = t;
@@ -1612,7 +1706,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     // A leaf pass whose other-kind lanes all sit at one leaf (the Cornell box:
                     // always, with single node steps) tests it with scalar loads.
                     const uint32_t r0 = __builtin_amdgcn_readfirstlane(ref);
-                    const bool uni = __builtin_amdgcn_ballot_w64(ref != r0) == 0;
+#ifndef GS_UNI_MN
+#define GS_UNI_MN 1
+#endif
+                    // (GS_UNI_MN 0: media / nested-BVH kernels without the scalar-load copy)
+                    const bool uni = (GS_UNI_MN || !(FEAT & (GS_FEAT_MEDIA | GS_FEAT_NESTED))) &&
+                                     __builtin_amdgcn_ballot_w64(ref != r0) == 0;
                     LeafHit lh;
                     if (uni) lh = leaf_other<FEAT, true>(sc, qs, r0, ray, tmin, closest, rng, s_cnt);
                     else lh = leaf_other<FEAT, false>(sc, qs, ref, ray, tmin, closest, rng, s_cnt);
@@ -1641,7 +1740,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     if ((FEAT & GS_FEAT_SPHLEAF) == 0 && (ref >> GS_REF_SHIFT) != GS_REF_SPHERE) break;
                     if constexpr ((FEAT & GS_FEAT_VISITS) != 0)
                         count_visit(P->visits, P->visit_leaf_base + (cur & ~THR_LEAF));
-                    c_sph++;
+                    count_sph();
                     double t;
                     if (sphere_accept(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
                         closest = t;
@@ -1653,6 +1752,20 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 }
                 GS_MARK("leaf_end");
             }
+#ifndef GS_REMAT_RC
+#define GS_REMAT_RC 1
+#endif
+#if GS_REMAT_RC
+            // Media / nested-BVH kernels: the certified test's ray constants are recomputed
+            // after a leaf pass (the same function of the same ray), so they are not live
+            // through leaf_other, whose medium and nested tests need the registers.
+            if constexpr ((FEAT & (GS_FEAT_MEDIA | GS_FEAT_NESTED)) != 0) {
+                if (leaf_pass) {
+                    const d3 inv = inv_of(ray.d);
+                    rc = make_cert(ray.o, inv);
+                }
+            }
+#endif
 #ifdef GS_STAMPS
             {
                 uint64_t tp1;
@@ -1799,12 +1912,19 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #endif
 #undef LD
 #undef LI
+#undef Tr
+#undef Tg
+#undef Tb
+#undef GS_TP
 
     // flush counters: LDS -> global, one atomic per counter per block
     atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
     atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
     __syncthreads();
-    if (threadIdx.x < C_N && P->counters) atomicAdd(&P->counters[threadIdx.x], s_cnt[threadIdx.x]);
+    // (the block's first C_N lanes: wave 0, where the lane is the thread index; the test is
+    // a wave-uniform mask taken at the start, so no thread-index register is kept to here)
+    const uint32_t lane_end = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    if (((flushers >> lane_end) & 1ull) && P->counters) atomicAdd(&P->counters[lane_end], s_cnt[lane_end]);
 }
 
 // Per-launch parameters reach device memory by a one-thread kernel on the caller's stream
@@ -2317,6 +2437,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     // pad0 = 0}, leaf {next, ABI ref, pad0 = 1}; THR_END ends a tree), and the device copy
     // of the instances points its node children at their tree's first record.
     std::vector<DNode> nodes;
+    std::vector<TNode> nrecs;  // nodes' f32 records (index-aligned)
+    bool nested_cert = true;
     std::vector<gs_instance> insts(s->instances, s->instances + s->n_instances);
     {
         std::unordered_map<uint32_t, uint32_t> start;  // node index -> first record
@@ -2350,6 +2472,17 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                 for (uint32_t k = first; k < end; k++) {
                     if (nodes[k].left == end) nodes[k].left = THR_END;
                     if (!nodes[k].pad0 && nodes[k].right == end) nodes[k].right = THR_END;
+                }
+                for (uint32_t k = first; k < end; k++) {  // the f32 records (nested_bvh)
+                    const DNode& n = nodes[k];
+                    if (n.pad0) {
+                        nrecs.push_back(TNode{0, 0, 0, 0, 0, 0, NREC_LEAF | n.left, n.right});
+                    } else {
+                        nrecs.push_back(TNode{(float)n.mnx, (float)n.mny, (float)n.mxx, (float)n.mxy, (float)n.mnz,
+                                              (float)n.mxz, n.left, n.right});
+                        for (double v : {n.mnx, n.mny, n.mnz, n.mxx, n.mxy, n.mxz})
+                            if (!(std::fabs(v) <= 1e15)) nested_cert = false;
+                    }
                 }
                 it = start.emplace(root, first).first;
             }
@@ -2552,6 +2685,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     }
     Layout L;
     size_t o_nodes = L.add(nodes.data(), nodes.size() * sizeof(DNode));
+    size_t o_nrecs = L.add(nrecs.data(), nrecs.size() * sizeof(TNode));
     size_t o_tnodes = L.add(tnodes.data(), tnodes.size() * sizeof(TNode));
     size_t o_tboxes = L.add(tboxes.data(), tboxes.size() * sizeof(TBox));
     size_t o_tleaves = L.add(tleaves.data(), tleaves.size() * sizeof(TLeaf));
@@ -2591,6 +2725,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     uint8_t* b = (uint8_t*)ds->mem;
     DevScene& d = ds->dev;
     d.nodes = (const DNode*)(b + o_nodes);
+    d.nrecs = (const TNode*)(b + o_nrecs);
+    d.nested_cert = nested_cert ? 1u : 0u;
     d.spheres = (const DSphere*)(b + o_sph);
     d.sphere_mat = (const uint32_t*)(b + o_sphm);
     d.mspheres = (const gs_msphere*)(b + o_msph);
@@ -2718,6 +2854,10 @@ int64_t gs_partition_capacity(const gs_camera* cam, const gs_partition* p) {
 }
 
 static void (*kernel_for(int feat))(KArgs) {
+#ifdef GS_ONLY_FEAT  // register-pressure experiments (tools/resource_usage.sh): one instantiation
+    (void)feat;
+    return gs_render_kernel<GS_ONLY_FEAT>;
+#else
     switch (feat) {
         case GS_FEAT_MEDIA: return gs_render_kernel<GS_FEAT_MEDIA>;
         case GS_FEAT_NESTED: return gs_render_kernel<GS_FEAT_NESTED>;
@@ -2744,6 +2884,7 @@ static void (*kernel_for(int feat))(KArgs) {
             return gs_render_kernel<GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_LDSTREE>;
         default: return gs_render_kernel<0>;
     }
+#endif
 }
 
 gs_status gs_render_tiles_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
@@ -2906,7 +3047,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         HIPCHK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
         // The node mirror must start at LDS address 0 (load_tnode): no static LDS.
         if (fa.sharedSizeBytes != 0) return fail(GS_ERR_UNSUPPORTED, "render kernel with static LDS");
-        const int64_t room = (int64_t)max_lds - (int64_t)lane_lds_bytes(chunked);
+        const int64_t room = (int64_t)max_lds - (int64_t)lane_lds_bytes(chunked, ds->feat);
         if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
         uint32_t ln = ds->lds_nodes, ll = ds->lds_leaves, lq = ds->lds_quads;
         auto bytes = [&] {
@@ -2921,7 +3062,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         lc.lds_nodes = ln;
         lc.lds_leaves = ll;
         lc.lds_quads = lq;
-        lc.lds = lane_lds_bytes(chunked) + (size_t)bytes();
+        lc.lds = lane_lds_bytes(chunked, ds->feat) + (size_t)bytes();
         lc.feat = ds->feat;
         if (ln < ds->node_records || ll < ds->leaf_records) lc.feat &= ~GS_FEAT_LDSTREE;
         int occ = 0;
@@ -2934,7 +3075,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     a.lds_nodes = lc.lds_nodes;
     a.lds_leaves = lc.lds_leaves;
     a.lds_quads = lc.lds_quads;
-    a.lane_nd = lane_nd(chunked);
+    a.lane_nd = lane_nd(chunked, ds->feat);
     const int per_cu = g_blocks_per_cu > 0 ? g_blocks_per_cu : lc.per_cu;
     int64_t blocks = (int64_t)cus * per_cu;
     // no more waves than work: one lane per item at most

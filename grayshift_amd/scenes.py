@@ -318,6 +318,9 @@ CONFIGS = {
 
 
 def config(name, width=None, spp=None):
-    """A BASELINE config; width/spp overrides give the small parity-test versions."""
+    """A BASELINE config; width/spp overrides give the small parity-test versions.  A
+    reference scene's name (SCENES) gives that scene at fixed spp (default 400 px, 64 spp)."""
+    if name not in CONFIGS and name in SCENES:
+        return SCENES[name](width=width or 400, settings=fixed_spp(spp or 64))
     scene, kw, w, s = CONFIGS[name]
     return SCENES[scene](width=width or w, settings=fixed_spp(spp or s), **kw)

@@ -1,0 +1,29 @@
+"""The code object that is timed is the one that was profiled.
+
+bench.py reads the PMC summary keyed by a hash of libgrayshift.so's gfx950 code objects
+(grayshift_amd/codeobj.py, profiles/pmc/<config>_<hash>.json).  The driver builds the
+library afresh from the sources, so (1) a clean rebuild must reproduce the hash of the
+in-tree build, and (2) the committed summaries must include the C4 one for that hash, or
+the driver's bench line would carry no roofline fraction.  No device needed."""
+import os
+import shutil
+
+from grayshift_amd import build, codeobj
+from grayshift_amd._native import LIB_PATH
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_clean_rebuild_reproduces_the_code_object_hash(built, tmp_path):
+    out = os.path.join(str(tmp_path), "rebuild.so")
+    try:
+        build.build_product(force=True, out=out)
+        assert codeobj.code_object_hash(out) == codeobj.code_object_hash(LIB_PATH)
+    finally:
+        shutil.rmtree(os.path.join(build.HERE, "csrc", "_obj_rebuild"), ignore_errors=True)
+
+
+def test_committed_pmc_summary_matches_the_built_code_object(built):
+    h = codeobj.code_object_hash(LIB_PATH)
+    path = os.path.join(ROOT, "profiles", "pmc", "C4_%s.json" % h)
+    assert os.path.exists(path), "no PMC summary for code object %s: run tools/pmc.sh and commit it" % h

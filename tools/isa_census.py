@@ -64,6 +64,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--feat", type=int, default=20)
     ap.add_argument("--dump", default=None, help="write the marked regions' assembly here")
+    ap.add_argument("--dump-kernel", default=None, help="write the whole instantiation's assembly here")
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as d:
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-x", "hip",
@@ -75,6 +76,8 @@ def main():
     i0 = next(i for i, l in enumerate(s) if l.startswith(name))
     i1 = next(i for i in range(i0, len(s)) if s[i].startswith(".Lfunc_end"))
     k = s[i0:i1]
+    if a.dump_kernel:
+        open(a.dump_kernel, "w").write("\n".join(k) + "\n")
     marks = {}
     for i, l in enumerate(k):
         m = re.search(r";; GS_MARK (\w+)", l)
@@ -83,7 +86,8 @@ def main():
     nb, ne = marks["node_begin"][0], marks["node_end"][0]
     fb, fe = marks["fallback_begin"][0], marks["fallback_end"][0]
     lb, le = marks["leaf_begin"][0], marks["leaf_end"][-1]
-    ob, oe = marks["other_begin"][0], marks["other_end"][0]
+    # sphere-only kernels (GS_FEAT_SPHLEAF) have no other-kind leaf region
+    ob, oe = (marks["other_begin"][0], marks["other_end"][0]) if "other_begin" in marks else (le, le)
     # the traversal loop header: the last "Loop Header" label before node_begin
     hdr = max(i for i in range(nb) if "Loop Header" in k[i] or "This Loop Header" in k[i])
     # The compiler spreads the f64 test's code (fallback and non-cert waves) over several

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--config", nargs="+", default=["C4"])
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--timeout", type=int, default=200)
+    ap.add_argument("--width", type=int, default=None, help="frame width (reference scenes; invalidates a metric config)")
+    ap.add_argument("--spp", type=int, default=None)
     a = ap.parse_args()
     out_dir = os.path.join(ROOT, "gpurun_out", "sweep")
     os.makedirs(out_dir, exist_ok=True)
@@ -36,6 +38,8 @@ def main():
         lib, config, vals = combo[0], combo[1], combo[2:]
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(a.steps), "--warmup", "1", "--no-cpu",
                "--config", config]
+        cmd += ["--width", str(a.width)] if a.width else []
+        cmd += ["--spp", str(a.spp)] if a.spp else []
         for k, v in zip(KNOBS, vals):
             if v is not None:
                 cmd += ["--" + k.replace("_", "-"), str(v)]
