@@ -237,17 +237,33 @@ __device__ __forceinline__ double lo_hi(unsigned int lo, unsigned int hi) { retu
 
 // A node record (2 x 16 B) at byte offset `off`: a = (mnx, mny, mxx, mxy), b = (mnz, mxz,
 // hit, miss).  (Offsets are u32: fewer than 2^26 records; leaf offsets i * 48 < 2^32.)
+//
+// Bank swizzle (GS_NODE_SWZ).  ds_read_b128 serves a wave in 4 groups of 16 lanes, each
+// lane's 16 B on 4 of the 64 banks, (a / 16) mod 16 picking the 4 (MI355X_MICROARCH.md,
+// LDS): with 32-B records every lane's first half lies on an even 4-bank group, so 16
+// lanes at different records share 8 groups.  The mirror stores an odd record's halves
+// swapped and a node link is the address of its record's first half (index << 5, plus 16
+// for an odd index): the first reads then spread over all 16 groups, and the second half
+// is at link ^ 16.  Global records keep their order (link & ~31).
+#ifndef GS_NODE_SWZ
+#define GS_NODE_SWZ 0  // measured: C4 -1.4%, C3 +0.7%, C5 -0.7% (profiles/r03/ab_node_swizzle_flush_rank.txt)
+#endif
+#ifndef GS_QUAD_SWZ
+#define GS_QUAD_SWZ 1
+#endif
+__host__ __device__ constexpr uint32_t node_link(uint32_t pos) { return (pos << 5) | (GS_NODE_SWZ ? (pos & 1u) << 4 : 0u); }
+__device__ __forceinline__ uint32_t node_half_b(uint32_t off) { return GS_NODE_SWZ ? off ^ 16u : off + 16u; }
+__device__ __forceinline__ uint32_t node_global(uint32_t off) { return GS_NODE_SWZ ? off & ~31u : off; }
 template <bool LDS_ONLY>
 __device__ __forceinline__ void load_tnode(const uint8_t* s_nodes, const TNode* g, uint32_t off, uint32_t lds_bytes,
                                            u32x4& a, u32x4& b) {
     if (LDS_ONLY || off < lds_bytes) {
         // The kernel has no static LDS (checked at launch), so the node mirror's first byte
         // is LDS address 0 and `off` is the record's LDS address (no address arithmetic).
-        lds_u32x4* q = (lds_u32x4*)(uintptr_t)off;
-        a = q[0];
-        b = q[1];
+        a = *(lds_u32x4*)(uintptr_t)off;
+        b = *(lds_u32x4*)(uintptr_t)node_half_b(off);
     } else {
-        const u32x4* q = reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(g) + off);
+        const u32x4* q = reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(g) + node_global(off));
         a = q[0];
         b = q[1];
     }
@@ -260,9 +276,8 @@ template <bool LDS_ONLY>
 __device__ __forceinline__ void load_tnode_w(const uint8_t* s_nodes, const TNode* g, uint32_t off, uint32_t lds_bytes,
                                              u32x4& a, u32x4& b) {
     if (LDS_ONLY || __builtin_expect(__builtin_amdgcn_ballot_w64(off >= lds_bytes) == 0, 1)) {
-        lds_u32x4* q = (lds_u32x4*)(uintptr_t)off;
-        a = q[0];
-        b = q[1];
+        a = *(lds_u32x4*)(uintptr_t)off;
+        b = *(lds_u32x4*)(uintptr_t)node_half_b(off);
     } else {
         load_tnode<false>(s_nodes, g, off, lds_bytes, a, b);
     }
@@ -383,7 +398,10 @@ __device__ __forceinline__ DNode ld_node_g(const DNode* p) {  // a nested-BVH no
 }
 template <bool UNI>
 __device__ __forceinline__ u32x4 quad_part(const QuadSrc& qs, uint32_t i, uint32_t k) {
-    if (!UNI && i < qs.n_lds) return ((lds_u32x4*)(qs.lds + i * (uint32_t)sizeof(TQuad)))[k];
+    // (the mirror stores quad i's 16-B chunk k at chunk k ^ (i & 7): 128-B records would put
+    // every lane's chunk k on the same 2 of ds_read_b128's 16 bank groups, GS_NODE_SWZ)
+    if (!UNI && i < qs.n_lds)
+        return *(lds_u32x4*)(qs.lds + i * (uint32_t)sizeof(TQuad) + ((GS_QUAD_SWZ ? (k ^ (i & 7u)) : k) << 4));
     return sp<UNI>(reinterpret_cast<const u32x4*>(qs.g + i))[k];
 }
 template <bool UNI>
@@ -1117,13 +1135,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     {
         const uint4* src = reinterpret_cast<const uint4*>(A.tnodes);
         uint4* dst = reinterpret_cast<uint4*>(s_nodes);
-        for (uint32_t k = threadIdx.x; k < A.lds_nodes * 2u; k += GS_BLOCK) dst[k] = src[k];
+        // (record r's 16-B halves: swapped when r is odd, GS_NODE_SWZ)
+        for (uint32_t k = threadIdx.x; k < A.lds_nodes * 2u; k += GS_BLOCK) dst[GS_NODE_SWZ ? k ^ ((k >> 1) & 1u) : k] = src[k];
         src = reinterpret_cast<const uint4*>(A.tleaves);
         dst = reinterpret_cast<uint4*>(s_leaves);
         for (uint32_t k = threadIdx.x; k < A.lds_leaves * 3u; k += GS_BLOCK) dst[k] = src[k];
         src = reinterpret_cast<const uint4*>(A.tquads);
         dst = reinterpret_cast<uint4*>(s_quads);
-        for (uint32_t k = threadIdx.x; k < A.lds_quads * 8u; k += GS_BLOCK) dst[k] = src[k];
+        for (uint32_t k = threadIdx.x; k < A.lds_quads * 8u; k += GS_BLOCK) dst[GS_QUAD_SWZ ? k ^ ((k >> 3) & 7u) : k] = src[k];
     }
     const QuadSrc qs{s_quads, A.tquads, A.lds_quads};
     // Per-lane pixel / path state after the mirror: [L_ND][GS_BLOCK] f64, [L_NI][GS_BLOCK] u32.
@@ -1247,7 +1266,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             flush_counts();
         }
 #endif
-        if ((c_nodes | c_sph) >= (1u << 30)) flush_counts();
+#ifndef GS_FLUSH_PER_ITEM
+#define GS_FLUSH_PER_ITEM 0
+#endif
+        if (GS_FLUSH_PER_ITEM || (c_nodes | c_sph) >= (1u << 30)) flush_counts();
         st = S_NEED;
     };
 
@@ -1381,8 +1403,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             const uint32_t tile_px = (uint32_t)(P->tile_w * P->tile_h);
             const bool blocked8 = (P->tile_w % 8 == 0) && (P->tile_h % 8 == 0);
             // set bits of `need` below this lane (v_mbcnt: no 64-bit lane mask kept live)
+            // (media / nested / sphere-only kernels; the others keep the popcount of the
+            // masked ballot: C3 +0.6%, C5 +1.2%, C4 -0.3% the other way round)
+#ifndef GS_RANK_MBCNT
+#define GS_RANK_MBCNT ((FEAT & (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_SPHLEAF)) != 0)
+#endif
             const uint32_t rank =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                GS_RANK_MBCNT ? __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u))
+                              : (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
             if (st == S_NEED && rank < take) {
                 const uint64_t q = (uint64_t)base + (uint64_t)rank;
                 if (q >= P->n_items) {
@@ -1544,9 +1572,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     // base), the box test, and the next record: the hit link or the miss link.
                     u32x4 ra, rb;
                     if constexpr (LDSP) {
-                        lds_u32x4* q = (lds_u32x4*)(uintptr_t)cur;
-                        ra = q[0];
-                        rb = q[1];
+                        ra = *(lds_u32x4*)(uintptr_t)cur;
+                        rb = *(lds_u32x4*)(uintptr_t)node_half_b(cur);
                     } else {
                         load_tnode_w<(FEAT & GS_FEAT_LDSTREE) != 0>(s_nodes, A.tnodes, cur, A.lds_nodes << 5, ra, rb);
                     }
@@ -1756,10 +1783,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #define GS_REMAT_RC 1
 #endif
 #if GS_REMAT_RC
-            // Media / nested-BVH kernels: the certified test's ray constants are recomputed
-            // after a leaf pass (the same function of the same ray), so they are not live
-            // through leaf_other, whose medium and nested tests need the registers.
-            if constexpr ((FEAT & (GS_FEAT_MEDIA | GS_FEAT_NESTED)) != 0) {
+            // Nested-BVH kernels and media kernels with sphere leaf runs: the certified test's
+            // ray constants are recomputed after a leaf pass (the same function of the same
+            // ray), so they are not live through leaf_other, whose medium and nested tests
+            // need the registers (without it these spill 12-36 B/lane).  Media-only kernels
+            // (cornell_smoke: a leaf pass after nearly every single node step) have the
+            // registers and skip the recomputation (with it: -6.6%).
+            if constexpr ((FEAT & GS_FEAT_NESTED) != 0 ||
+                          (FEAT & (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)) == (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)) {
                 if (leaf_pass) {
                     const d3 inv = inv_of(ray.d);
                     rc = make_cert(ray.o, inv);
@@ -2173,7 +2204,7 @@ static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* 
     out.tnodes.resize(nt_rest);
     out.tboxes.resize(nt_rest);
     out.tleaves.resize(nl_rest);
-    auto tag = [&](uint32_t l) { return l >= n ? THR_END : (t.leaf[l] ? (THR_LEAF | pos[l]) : pos[l] << 5); };
+    auto tag = [&](uint32_t l) { return l >= n ? THR_END : (t.leaf[l] ? (THR_LEAF | pos[l]) : node_link(pos[l])); };
     for (uint32_t i = 0; i < n; i++) {
         const DNode& r = t.rec[i];
         if (t.leaf[i]) {
