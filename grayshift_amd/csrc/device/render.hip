@@ -249,7 +249,7 @@ __device__ __forceinline__ double lo_hi(unsigned int lo, unsigned int hi) { retu
 #define GS_NODE_SWZ 0  // measured: C4 -1.4%, C3 +0.7%, C5 -0.7% (profiles/r03/ab_node_swizzle_flush_rank.txt)
 #endif
 #ifndef GS_QUAD_SWZ
-#define GS_QUAD_SWZ 1
+#define GS_QUAD_SWZ 0  // measured: final_scene +0.2%, C3 +0.5%, C5 -1.3% (profiles/r03/ab_quad_swizzle.txt)
 #endif
 __host__ __device__ constexpr uint32_t node_link(uint32_t pos) { return (pos << 5) | (GS_NODE_SWZ ? (pos & 1u) << 4 : 0u); }
 __device__ __forceinline__ uint32_t node_half_b(uint32_t off) { return GS_NODE_SWZ ? off ^ 16u : off + 16u; }

@@ -15,7 +15,7 @@ for sc in ${SCENES:-final_scene cornell_smoke perlin_spheres simple_light}; do
       > $O/$sc.json 2> $O/$sc.err || { echo "$sc failed"; tail -5 $O/$sc.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('%-16s %9.1f Msamples/s %9.1f ms kernel %9.1f ms rays %d' % (sys.argv[2], d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['config']['rays_per_frame']))" $O/$sc.json $sc
 done
-if [ -n "${PROF:-final_scene}" ]; then
+if [ "${NOPROF:-0}" != 1 ]; then
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_${PROF:-final_scene} -o run -- \
       python3 $R/bench.py --config ${PROF:-final_scene} --width $W --spp $S --steps 1 --warmup 1 --no-cpu \
       > $O/prof.json 2> $O/prof.err || { echo "prof failed"; tail -5 $O/prof.err; exit 1; }
