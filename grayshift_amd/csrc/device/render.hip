@@ -111,6 +111,11 @@ struct alignas(16) DMaterial {
 };
 
 enum { C_RAYS = 0, C_NODES, C_SPH, C_MSPH, C_QUAD, C_TRI, C_INST, C_LIST, C_HITS, C_IMG, C_HDRI, C_PATHS, C_PIX, C_MED, C_NOISE, C_N };
+#ifdef GS_CERT_CHECK
+#define GS_CNT_SLOTS (C_N + 1)  // + slot 15: nested certified-decision mismatches
+#else
+#define GS_CNT_SLOTS C_N
+#endif
 
 struct DevScene {
     const DNode* nodes;   // nested trees' records with their f64 boxes (the f64 test)
@@ -589,6 +594,12 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
                 h = box_cert(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(b.x), __uint_as_float(a.z),
                              __uint_as_float(a.w), __uint_as_float(b.y), c, 0.001f, closest32, undecided);
             if (undecided) h = box_hit_v(ld_node_g(sc.nodes + cur), r.o, inv_of(r.d), tmin, closest);
+#ifdef GS_CERT_CHECK
+            // diagnostic build: every certified nested decision re-checked in f64; mismatches
+            // counted in the block's slot 15 (flushed to counters[15], tools/diag_cert.py)
+            if (fast && !undecided && box_hit_v(ld_node_g(sc.nodes + cur), r.o, inv_of(r.d), tmin, closest) != h)
+                atomicAdd(&cnt[15], 1ull);
+#endif
             cur = h ? b.z : b.w;
         }
     }
@@ -1153,7 +1164,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     unsigned long long* s_reg = s_cnt + 16;  // [(GS_BLOCK / 64) * 8]
     if (threadIdx.x < (GS_BLOCK / 64) * 8) s_reg[threadIdx.x] = 0;
 #endif
-    if (threadIdx.x < C_N) s_cnt[threadIdx.x] = 0;
+    if (threadIdx.x < GS_CNT_SLOTS) s_cnt[threadIdx.x] = 0;
     __syncthreads();
 
     const KParams* __restrict__ P = A.P;
@@ -1161,7 +1172,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     const gs_camera& cam = P->cam;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t tid = threadIdx.x;
-    const uint64_t flushers = __builtin_amdgcn_ballot_w64(tid < C_N);  // the counters' flushing lanes
+    const uint64_t flushers = __builtin_amdgcn_ballot_w64(tid < GS_CNT_SLOTS);  // the counters' flushing lanes
     const double tmin = 0.001;
 #ifndef GS_NESTED_SITES
 #define GS_NESTED_SITES 1
@@ -1661,6 +1672,23 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 uint32_t next, ref;
                 load_tleaf<(FEAT & GS_FEAT_LDSTREE) != 0>(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr,
                                                          next, ref);
+#ifndef GS_LEAF_KIND_BATCH
+#define GS_LEAF_KIND_BATCH 0
+#endif
+                // Kind-batched leaf passes (GS_LEAF_KIND_BATCH): besides stationary spheres, a
+                // pass tests only the leaves of one other kind (the first such lane's); lanes
+                // at other kinds keep their leaf for a later pass, so each kind's code runs
+                // with its lanes together instead of every kind present running in turn.
+                bool take_leaf = true;
+                if constexpr (GS_LEAF_KIND_BATCH && (FEAT & GS_FEAT_SPHLEAF) == 0) {
+                    const uint32_t kind = ref >> GS_REF_SHIFT;
+                    const uint64_t om = __builtin_amdgcn_ballot_w64(kind != GS_REF_SPHERE);
+                    if (om != 0) {
+                        const uint32_t k0 = __builtin_amdgcn_readlane(kind, (uint32_t)__builtin_ctzll(om));
+                        take_leaf = kind == GS_REF_SPHERE || kind == k0;
+                    }
+                }
+                if (take_leaf) {
                 if constexpr ((FEAT & GS_FEAT_VISITS) != 0) count_visit(P->visits, P->visit_leaf_base + (cur & ~THR_LEAF));
 #ifdef GS_STAMPS
                 {  // counted by the pass's first active lane (summed over lanes at the end)
@@ -1777,6 +1805,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                     cur = next;
                 }
+                }  // take_leaf
                 GS_MARK("leaf_end");
             }
 #ifndef GS_REMAT_RC

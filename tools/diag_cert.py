@@ -11,7 +11,7 @@ from grayshift_amd.scene import fixed_spp
 name = sys.argv[1] if len(sys.argv) > 1 else "final_scene"
 # a BASELINE config at its full size and spp (or width / spp given after it), else a scene
 # at 40 px, 8 spp
-if name in scenes.CONFIGS:
+if name in scenes.CONFIGS or len(sys.argv) > 3:
     kw = {"width": int(sys.argv[2]), "spp": int(sys.argv[3])} if len(sys.argv) > 3 else {}
     sc = scenes.config(name, **kw)
 else:
