@@ -1672,13 +1672,17 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 uint32_t next, ref;
                 load_tleaf<(FEAT & GS_FEAT_LDSTREE) != 0>(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr,
                                                          next, ref);
-#ifndef GS_LEAF_KIND_BATCH
-#define GS_LEAF_KIND_BATCH 0
-#endif
                 // Kind-batched leaf passes (GS_LEAF_KIND_BATCH): besides stationary spheres, a
                 // pass tests only the leaves of one other kind (the first such lane's); lanes
                 // at other kinds keep their leaf for a later pass, so each kind's code runs
-                // with its lanes together instead of every kind present running in turn.
+                // with its lanes together instead of every kind present running in turn.  On
+                // for kernels with BVHs under instances or staged shading, where many kinds
+                // meet: final_scene +8.5%, C5 +1.3%; off elsewhere (C3 -1.2%, cornell_smoke
+                // -0.4%; profiles/r03/ab_leaf_kind_batch.txt).  Each lane still tests its own
+                // leaves in its own order, so nothing it computes changes.
+#ifndef GS_LEAF_KIND_BATCH
+#define GS_LEAF_KIND_BATCH ((FEAT & (GS_FEAT_NESTED | GS_FEAT_MIXED)) != 0)
+#endif
                 bool take_leaf = true;
                 if constexpr (GS_LEAF_KIND_BATCH && (FEAT & GS_FEAT_SPHLEAF) == 0) {
                     const uint32_t kind = ref >> GS_REF_SHIFT;
