@@ -2055,7 +2055,15 @@ static thread_local std::string tl_err;
 static int32_t g_shade_batch = 52;  // swept on MI355X C4 (chunked, uniform loop): 48 -> 3502, 52 -> 3535-3568, 56 -> 3506-3536 Msamples/s
 static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
 static int32_t g_node_steps = 0;  // 0: the scene's own (gs_device_scene.node_steps)
-static int32_t g_leaf_batch = 12;  // swept on MI355X C4 with leaf runs: 8 -> 4586, 10 -> 4632, 12 -> 4648-4651, 14 -> 4624, 16 -> 4592
+// leaf batch: 0 = the scene's choice (12: swept on MI355X C4 with leaf runs: 8 -> 4586, 10 ->
+// 4632, 12 -> 4648-4651, 14 -> 4624, 16 -> 4592; GS_KIND_LEAF_BATCH for kind-batched kernels)
+static int32_t g_leaf_batch = 0;
+#ifndef GS_KIND_LEAF_BATCH
+#define GS_KIND_LEAF_BATCH 48
+#endif
+#ifndef GS_KIND_NODE_STEPS
+#define GS_KIND_NODE_STEPS 3
+#endif
 // Bytes of threaded records mirrored in LDS per block (the most-tested ones): what is
 // left of the block's share of the CU's 160 KiB (4 waves/SIMD = 1024 lanes per CU) after
 // the lane state.  -1 = that budget; >= 0 explicit (A/B).
@@ -2130,6 +2138,7 @@ struct gs_device_scene {
     uint32_t thr_root = THR_END;
     uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0;  // mirrored prefixes (per block)
     int32_t node_steps = GS_NODE_STEPS;      // node steps per node pass (from the tree's shape)
+    int32_t leaf_batch = 12;                 // lanes at a leaf before a leaf pass (scene's choice)
     uint32_t node_records = 0, leaf_records = 0;
     double nodes_per_leaf = 0.0, other_leaf_frac = 0.0;
     // Launch state, mutated by launches of a const scene: guarded by `mu`.
@@ -2848,6 +2857,14 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     if (sph_leaves && leaf_runs && !(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED))) ds->feat |= GS_FEAT_SPHLEAF;
     ds->cert_boxes = cert_boxes;
     ds->node_steps = auto_node_steps;
+    // Kernels with kind-batched leaf passes (nested BVHs, staged shading) gather more lanes
+    // per leaf pass, of which each pass serves one kind, and step nodes in passes of 3:
+    // final_scene 1440^2 x 64 spp (leaf batch, node steps) (12, 1) 1206 -> (32, 3) 1540 ->
+    // see GS_KIND_LEAF_BATCH (profiles/r03/sweep_final_scene_leaf_batch.txt, sweep_*).
+    if ((ds->feat & (GS_FEAT_NESTED | GS_FEAT_MIXED)) && !(ds->feat & GS_FEAT_SPHLEAF)) {
+        ds->leaf_batch = GS_KIND_LEAF_BATCH;
+        ds->node_steps = std::max<int32_t>(ds->node_steps, GS_KIND_NODE_STEPS);
+    }
     ds->tree = std::move(tree_keep);
     ds->pos = std::move(placed_pos);
     ds->n_quads = s->n_quads;
@@ -3095,7 +3112,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     a.root = ds->thr_root;
     a.cert_boxes = ds->cert_boxes ? 1 : 0;
     a.shade_batch = g_shade_batch;
-    a.leaf_batch = g_leaf_batch < 1 ? 1 : g_leaf_batch;  // 0 would never step a node
+    a.leaf_batch = std::max<int32_t>(1, g_leaf_batch > 0 ? g_leaf_batch : ds->leaf_batch);  // (0 would never step a node)
     a.node_steps = std::max(1, std::min<int32_t>(GS_NODE_STEPS, g_node_steps > 0 ? g_node_steps : ds->node_steps));
     gs_device_scene* mds = const_cast<gs_device_scene*>(ds);
     std::lock_guard<std::mutex> lock(mds->mu);

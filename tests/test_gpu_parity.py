@@ -225,10 +225,10 @@ class _chunk:
         self.n = n
 
     def __enter__(self):
-        g.set_tuning(52, 0, 12, self.n)
+        g.set_tuning(52, 0, 0, self.n)
 
     def __exit__(self, *a):
-        g.set_tuning(52, 0, 12, -1)
+        g.set_tuning(52, 0, 0, -1)
 
 
 @pytest.mark.parametrize("name", ["C4", "C3", "earth_fixed"])
