@@ -2062,7 +2062,7 @@ static int32_t g_leaf_batch = 0;
 #define GS_KIND_LEAF_BATCH 48
 #endif
 #ifndef GS_KIND_NODE_STEPS
-#define GS_KIND_NODE_STEPS 3
+#define GS_KIND_NODE_STEPS 8
 #endif
 // Bytes of threaded records mirrored in LDS per block (the most-tested ones): what is
 // left of the block's share of the CU's 160 KiB (4 waves/SIMD = 1024 lanes per CU) after
@@ -2857,11 +2857,12 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     if (sph_leaves && leaf_runs && !(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED))) ds->feat |= GS_FEAT_SPHLEAF;
     ds->cert_boxes = cert_boxes;
     ds->node_steps = auto_node_steps;
-    // Kernels with kind-batched leaf passes (nested BVHs, staged shading) gather more lanes
-    // per leaf pass, of which each pass serves one kind, and step nodes in passes of 3:
-    // final_scene 1440^2 x 64 spp (leaf batch, node steps) (12, 1) 1206 -> (32, 3) 1540 ->
-    // see GS_KIND_LEAF_BATCH (profiles/r03/sweep_final_scene_leaf_batch.txt, sweep_*).
-    if ((ds->feat & (GS_FEAT_NESTED | GS_FEAT_MIXED)) && !(ds->feat & GS_FEAT_SPHLEAF)) {
+    // Scenes with BVHs under instances (kind-batched leaf passes over many leaf kinds) gather
+    // more lanes per leaf pass, each pass serving one kind, and step nodes in full passes:
+    // final_scene 1440^2 x 64 spp, (leaf batch, node steps): (12, 1) 1206, (32, 3) 1540,
+    // (48, 3) 1594, (48, 8) 1679, (64, 8) 1662 Msamples/s (profiles/r03/sweep_final_scene_
+    // leaf_batch*.txt).  Not for staged shading alone: C5 leaf batch 12 6178, 24 5989, 48 5236.
+    if (ds->feat & GS_FEAT_NESTED) {
         ds->leaf_batch = GS_KIND_LEAF_BATCH;
         ds->node_steps = std::max<int32_t>(ds->node_steps, GS_KIND_NODE_STEPS);
     }

@@ -215,8 +215,8 @@ int32_t gs_version(void);
 /* Launch tuning, process-wide: shade_batch in [1, 64] = finished lanes a wave
  * collects before it shades them together; blocks_per_cu in [0, 8], 0 = from the
  * occupancy query; leaf_batch in [0, 64] = lanes waiting at a leaf before the wave
- * runs a leaf-test pass (0 = the scene's own choice: 12, or more for scenes whose
- * kernels batch leaf passes by kind, i.e. with BVHs under instances or staged shading);
+ * runs a leaf-test pass (0 = the scene's own choice: 12, or 48 for scenes with BVHs
+ * under instances, whose leaf passes serve one leaf kind each);
  * sample_chunk = samples per work item when the settings run a single batch
  * (max_samples < batch_size, as every fixed-spp render): -1 auto (16, or batch/64 for
  * big batches: at most 64 chunks per pixel, and at most 4 GiB of chunk sums; ABI 7: the
