@@ -84,3 +84,26 @@ def test_final_scene_partition_invariance():
 def test_final_scene_ppm_matches_oracle():
     sc = scenes.final_scene(width=32, settings=fixed_spp(4))
     assert g.render_ppm(sc, seed=9)[0] == oracle.render_ppm(sc, seed=9)[0]
+
+
+def test_final_scene_is_independent_of_leaf_batch_and_node_steps():
+    """The scene's launch choices (leaf batch 48 and full node passes for BVHs under
+    instances, kind-batched leaf passes) only regroup which lanes a pass serves: every lane
+    tests its own records in its own order, so frames and counters equal any other
+    choice's, and the oracle's."""
+    from grayshift_amd import _native as N
+    sc = scenes.final_scene(width=40, settings=fixed_spp(4))
+    ref, rc = oracle.render(sc, seed=5)
+    runs = []
+    try:
+        for lb, ns in [(0, 0), (1, 1), (12, 3), (64, 8)]:
+            g.set_tuning(52, 0, lb, -1)
+            N.check(N.lib.gs_set_node_steps(ns))
+            runs.append(g.render(sc, seed=5))
+    finally:
+        g.set_tuning(52, 0, 0, -1)
+        N.check(N.lib.gs_set_node_steps(0))
+    for out, gc in runs:
+        assert np.array_equal(out, runs[0][0]) and gc == runs[0][1]
+    assert maxdiff(runs[0][0], ref) < TOL
+    assert counters_match(runs[0][1], rc)
