@@ -66,6 +66,14 @@ VALU_CYCLES = {"ADD_F32": 2, "MUL_F32": 2, "FMA_F32": 2, "TRANS_F32": 8, "ADD_F6
 PARITY_TOL = 1e-3  # north star: per-channel |delta| < 1e-3 vs the CPU path at a fixed seed
 
 
+def settings_desc(ss):
+    """'512 spp' for fixed-spp settings (one batch, camera.rs:158), else the adaptive ones."""
+    if ss.tolerance == 0.0 and ss.max_samples < ss.batch_size:
+        return "%d spp" % ss.batch_size
+    return "adaptive (confidence %g, tolerance %g, batch %d, max %d)" % (ss.confidence, ss.tolerance, ss.batch_size,
+                                                                        ss.max_samples)
+
+
 def algorithmic_bytes(c):
     return sum(BYTES[k] * int(c[k]) for k in BYTES)
 
@@ -89,6 +97,8 @@ def parse():
     ap.add_argument("--leaf-batch", type=int, default=None)
     ap.add_argument("--node-steps", type=int, default=0, help="node steps per node pass (0: the scene's choice)")
     ap.add_argument("--sample-chunk", type=int, default=None, help="samples per work item (-1 auto, 0 whole pixel)")
+    ap.add_argument("--adaptive-mode", type=int, default=1, choices=[0, 1],
+                    help="adaptive settings: 1 batch rounds (default), 0 the per-lane loop (gs_set_adaptive_mode)")
     ap.add_argument("--cpu-stride", type=int, default=3,
                     help="CPU baseline / parity subset at N=1: every Nth row and column")
     ap.add_argument("--parity-stride", type=int, default=12, help="parity subset at N>1: every Nth row and column")
@@ -123,6 +133,7 @@ def load_scene(a):
     g.set_tuning(a.shade_batch or 52, a.blocks_per_cu or 0, 0 if a.leaf_batch is None else a.leaf_batch,
                  -1 if a.sample_chunk is None else a.sample_chunk)
     g._native.check(g._native.lib.gs_set_node_steps(a.node_steps))
+    g._native.check(g._native.lib.gs_set_adaptive_mode(a.adaptive_mode))
     if a.config in scenes.CONFIGS:
         return scenes.config(a.config, width=a.width, spp=a.spp)
     a.width, a.spp = a.width or 400, a.spp or 64
@@ -309,8 +320,8 @@ def emit(a, sc, r, c, elapsed, kernel_avg_ms, img, world, launch_info):
     invalid = a.width is not None or a.spp is not None
     info = r.scene_info() if hasattr(r, "scene_info") else None
     cfg = {
-        "workload": "%s: %s %dx%d, %d spp%s" % (a.config, sc.name, r.width, r.height, sc.settings.batch_size,
-                                              " (OVERRIDDEN: not the metric)" if invalid else ""),
+        "workload": "%s: %s %dx%d, %s%s" % (a.config, sc.name, r.width, r.height, settings_desc(sc.settings),
+                                          " (OVERRIDDEN: not the metric)" if invalid else ""),
         "tile": a.tile, "parallelism": "tiles%d" % world,
     }
     cfg.update(launch_info)
@@ -434,8 +445,8 @@ def cpu_check(sc, a, img, stride, runs):
               "bit_identical_frac": round(float((gpu == ref.astype(np.float64)).mean()), 6),
               "pass": bool(d.max() < PARITY_TOL)}
     cpu = {"value": round(cnt["rays"] / med / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
-           "sample": "%d px (every %dth row/col of the frame) x %d spp = %d rays; render only (world/BVH build "
-                     "excluded), median of %d: %s s" % (len(sub), stride, sc.settings.batch_size, cnt["rays"],
+           "sample": "%d px (every %dth row/col of the frame) x %s = %d rays; render only (world/BVH build "
+                     "excluded), median of %d: %s s" % (len(sub), stride, settings_desc(sc.settings), cnt["rays"],
                                                         len(times), ", ".join("%.2f" % t for t in times))}
     return cpu, parity
 

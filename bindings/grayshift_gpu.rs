@@ -25,7 +25,7 @@ pub const GS_REF_TRIANGLE: u32 = 5;
 pub const GS_REF_LIST: u32 = 6;
 pub const GS_REF_INSTANCE: u32 = 7;
 pub const GS_REF_MEDIUM: u32 = 8;
-pub const GS_ABI_VERSION: i32 = 7;
+pub const GS_ABI_VERSION: i32 = 8;
 pub const fn gs_make_ref(kind: u32, idx: u32) -> u32 { (kind << GS_REF_SHIFT) | (idx & 0x0FFF_FFFF) }
 
 #[repr(C)] #[derive(Clone, Copy, Default)]
@@ -149,6 +149,7 @@ extern "C" {
     pub fn gs_debug_set_partial_budget(bytes: u64) -> gs_status;
     pub fn gs_set_node_steps(node_steps: i32) -> gs_status;
     pub fn gs_set_placement(mode: i32) -> gs_status;
+    pub fn gs_set_adaptive_mode(mode: i32) -> gs_status;
     pub fn gs_debug_record_visits(scene: *const gs_device_scene, cam: *const gs_camera, ss: *const gs_sample_settings,
                                   seed: u64, part: *const gs_partition, d_packed_rgb: *mut f32, d_visits: *mut u32,
                                   stream: *mut c_void) -> gs_status;

@@ -61,6 +61,14 @@ using namespace gsd;
 #define GS_MIN_WAVES 4
 #endif
 #define GS_MAX_CHAIN 4
+// Device-only ref kind: a HittableList of consecutive quads, [first, first + count), first <
+// 2^22, count < 64 (index bits: first | count << 22).  0 disables the rewrite (A/B).
+#ifndef GS_QRUN
+#define GS_QRUN 0
+#endif
+#define DREF_QRUN 9u
+#define QRUN_COUNT_SHIFT 22u
+#define QRUN_FIRST_MASK ((1u << QRUN_COUNT_SHIFT) - 1u)
 #define GS_NESTED_STACK 32  // max depth of a BVH under a Translate/RotateY chain (validation bound: the walk is stackless)
 // Kernel feature flags (template argument): scenes without them compile the code out.
 #define GS_FEAT_MEDIA 1   // ConstantMedium leaves (RNG draws inside traversal)
@@ -178,6 +186,21 @@ struct KParams {
     // per leaf record position from visit_leaf_base
     uint32_t* visits;
     uint32_t visit_leaf_base, pad1;
+    // Adaptive settings in batch rounds (per_sample = 1; DESIGN.md §3.2 "Adaptive sampling in
+    // batch rounds"): launch (round, segment) renders batch `round` of the active packed
+    // pixels active[seg_base, seg_base + seg_n), work item q = (entry q / cpp, samples
+    // [(q % cpp) * chunk, +chunk) of the batch), and every sample's colour goes to
+    // partial[(j * seg_n + entry) * 3] (sample-major: j = the sample's index in the batch);
+    // gs_round_combine_kernel then folds each pixel's batch into its running sums in sample
+    // order (camera.rs:138-147), takes the stop test (:149-164) and lists the pixels that go
+    // on.  gs_round_params_kernel sets the per-round fields from the device-side counts.
+    uint32_t per_sample, round_base, seg_base, seg_n;
+    uint32_t waves, lanes, pad2, pad3;
+    const uint32_t* active;    // this round's active packed pixels
+    uint32_t* next_active;     // the next round's, appended by the combine
+    uint32_t* active_buf[2];   // the two lists (rounds alternate)
+    uint32_t* round_counts;    // [rounds + 1]: active pixels per round
+    double* pstate;            // per packed pixel: the running Σr, Σg, Σb, Σlum, Σlum² (camera.rs:131-146)
 };
 
 // Hot kernel arguments: what the traversal loop reads every step.
@@ -493,6 +516,9 @@ __device__ __forceinline__ uint32_t walk_chain(const DevScene& sc, uint32_t cur,
 }
 
 // A HittableList (hittable.rs:71-86: shrinking closest) or one primitive.
+// A device-side QRUN ref (DREF_QRUN, set at upload: render.hip qrun_ref) is a list whose
+// members are the quads [first, first + count) in order (every Quad::cube, quad.rs:54-80),
+// so neither the list record nor its member refs are read: the same quads in the same order.
 template <bool UNI>
 __device__ __forceinline__ void shape_test(const DevScene& sc, const QuadSrc& qs, uint32_t cur, const Ray& r,
                                            double tmin, double closest, uint32_t inst_ref, LeafHit& res,
@@ -1087,6 +1113,16 @@ __device__ __forceinline__ void count_visit(uint32_t* counts, uint32_t idx) {
 #define GS_STAMP(t) do { } while (0)
 #define GS_REGION(k, t0) do { } while (0)
 #endif
+// Diagnostic builds (-DGS_WATCHDOG=N; on in the stamps build): a wave whose traversal phase
+// takes more than N passes, or whose loop more than 64 N iterations, prints every lane's
+// state once (the first 4 such waves of the launch) and retires its lanes, so a loop that
+// does not end names itself instead of running into the caller's time limit.
+#if defined(GS_STAMPS) && !defined(GS_WATCHDOG)
+#define GS_WATCHDOG (1 << 20)
+#endif
+#ifdef GS_WATCHDOG
+__device__ unsigned int g_wd_trips;
+#endif
 
 
 // Per-lane pixel state lives in LDS ([field][lane], conflict-free), touched once per
@@ -1234,9 +1270,17 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 
     // camera.rs:142-146 for one finished sample of colour L
     auto add_sample = [&](double Lr, double Lg, double Lb) {
-        LD(L_CSR) += Lr;
-        LD(L_CSG) += Lg;
-        LD(L_CSB) += Lb;
+        if (P->per_sample) {  // batch rounds: the sample's colour, summed in order by the combine
+            double* o = P->partial + (size_t)LI(L_ITEM) * 3;
+            o[0] = Lr;
+            o[1] = Lg;
+            o[2] = Lb;
+            LI(L_ITEM) += P->seg_n;
+        } else {
+            LD(L_CSR) += Lr;
+            LD(L_CSG) += Lg;
+            LD(L_CSB) += Lb;
+        }
         if (!P->chunk) {  // a chunk never reaches the stop test: Σlum, Σlum² unused
             double lum = 0.299 * Lr + 0.587 * Lg + 0.144 * Lb;
             LD(L_LSUM) += lum;
@@ -1267,10 +1311,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     };
     auto end_chunk = [&]() {
         const uint32_t item = LI(L_ITEM);
-        double* o = P->partial + (size_t)item * 3;
-        o[0] = LD(L_CSR);
-        o[1] = LD(L_CSG);
-        o[2] = LD(L_CSB);
+        if (!P->per_sample) {
+            double* o = P->partial + (size_t)item * 3;
+            o[0] = LD(L_CSR);
+            o[1] = LD(L_CSG);
+            o[2] = LD(L_CSB);
+        }
 #if !defined(GS_STAMPS) && !defined(GS_CERT_CHECK)  // (those builds use item_visits as their record buffer)
         if (P->item_visits) {
             atomicAdd(&P->item_visits[item / P->cpp], c_nodes);
@@ -1374,10 +1420,35 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     // stamps build: node steps (lanes) from global memory; wave node steps with any active lane,
     // with any lane reading its record from global memory; active lanes over those steps
     uint64_t d_gvis = 0, d_wsteps = 0, d_wsteps_g = 0, d_wlanes = 0;
+#ifdef GS_WATCHDOG
+    uint32_t wd_loop = 0;
+    // prints the lane's state (once per tripped wave, the launch's first 4) and retires the lane
+    auto wd_trip = [&](const char* where, uint32_t count) {
+        uint32_t k = 0;
+        if (lane == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) k = atomicAdd(&g_wd_trips, 1u);
+        k = __builtin_amdgcn_readfirstlane(k);
+        if (k < 4)
+            printf("GS_WATCHDOG %s n=%u block=%u wave=%u lane=%u st=%u cur=%08x fast=%d closest=%g hit_ref=%08x "
+                   "depth=%u bleft=%u item=%u sample=%u res_cnt=%u qdone=%d o=(%g %g %g) d=(%g %g %g)\n",
+                   where, count, (unsigned)blockIdx.x, (unsigned)(tid >> 6), lane, st, cur, (int)fast, closest,
+                   (uint32_t)hit_ref, LI(L_DEPTH), LI(L_BLEFT), LI(L_ITEM), LI(L_SAMPLE), res_cnt, (int)qdone, ray.o.x,
+                   ray.o.y, ray.o.z, ray.d.x, ray.d.y, ray.d.z);
+        st = S_DONE;
+        cur = THR_END;
+        fresh = false;
+        qdone = true;
+    };
+#endif
 #pragma unroll 1
     for (;;) {
         // ---------------------------------------------------------- refill
         GS_STAMP(ts0);
+#ifdef GS_WATCHDOG
+        if (++wd_loop > 64u * (uint32_t)GS_WATCHDOG) {
+            wd_trip("loop", wd_loop);
+            break;
+        }
+#endif
         // Refill and camera rays: lanes without an item take one (S_NEED -> S_CAM), then every
         // lane whose next sample needs a camera ray -- a new item's first, or the next sample
         // after the shade pass finished one -- runs advance() together, once per loop
@@ -1434,17 +1505,26 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     const uint32_t cpp = fine ? P->fine_cpp : P->cpp, csz = fine ? P->fine_chunk : P->chunk;
                     const uint32_t qr = fine ? q32 - P->fine_base : q32;
                     const uint32_t pr = udiv(qr, fine ? P->u_fcpp : P->u_cpp), ck = qr - pr * cpp;
-                    const uint32_t pq = fine ? P->fine_px + pr : pr;
-                    const uint32_t slot = udiv(pq, P->u_tpx), w = pq - slot * tile_px;
-                    uint32_t x, y;
-                    if (blocked8) {
-                        const uint32_t b = w >> 6, l = w & 63, bpr = (uint32_t)P->tile_w >> 3;
-                        const uint32_t by = udiv(b, P->u_bpr);
-                        x = (b - by * bpr) * 8 + (l & 7);
-                        y = by * 8 + (l >> 3);
-                    } else {
+                    uint32_t slot, x, y;
+                    if (P->per_sample) {  // batch rounds: the packed pixel of active entry pr
+                        const uint32_t it = P->active[P->seg_base + pr];
+                        slot = udiv(it, P->u_tpx);
+                        const uint32_t w = it - slot * tile_px;
                         y = udiv(w, P->u_tw);
                         x = w - y * (uint32_t)P->tile_w;
+                    } else {
+                        const uint32_t pq = fine ? P->fine_px + pr : pr;
+                        slot = udiv(pq, P->u_tpx);
+                        const uint32_t w = pq - slot * tile_px;
+                        if (blocked8) {
+                            const uint32_t b = w >> 6, l = w & 63, bpr = (uint32_t)P->tile_w >> 3;
+                            const uint32_t by = udiv(b, P->u_bpr);
+                            x = (b - by * bpr) * 8 + (l & 7);
+                            y = by * 8 + (l >> 3);
+                        } else {
+                            y = udiv(w, P->u_tw);
+                            x = w - y * (uint32_t)P->tile_w;
+                        }
                     }
                     const uint32_t item = slot * tile_px + y * (uint32_t)P->tile_w + x;
                     const uint32_t pos = (uint32_t)P->rank + slot * (uint32_t)P->world_size;
@@ -1472,7 +1552,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         LD(L_CSR) = 0.0;
                         LD(L_CSG) = 0.0;
                         LD(L_CSB) = 0.0;
-                        if (P->chunk) {
+                        if (P->per_sample) {
+                            // batch rounds: the sample slots of entry pr, samples ck * csz on
+                            LI(L_ITEM) = ck * csz * P->seg_n + pr;
+                            LI(L_SAMPLE) = P->round_base + ck * csz;
+                            LI(L_BLEFT) = min(csz, P->ss.batch_size - ck * csz);
+                        } else if (P->chunk) {
                             // chunk sums: a coarse pixel's at item * cpp, a fine one's after
                             // every coarse pixel's (the packed pixel and its queue position
                             // share a tile, so both are in the fine region or neither)
@@ -1525,8 +1610,17 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         // Invariant: cur != THR_END exactly for lanes whose ray is still being traced
         // (every other lane holds THR_END), so the loop reads lane states from `cur` alone
         // and only marks finished lanes S_SHADE once it ends.
+#ifdef GS_WATCHDOG
+        uint32_t wd_trav = 0;
+#endif
 #pragma unroll 1
         for (;;) {
+#ifdef GS_WATCHDOG
+            if (++wd_trav > (uint32_t)GS_WATCHDOG) {
+                wd_trip("traverse", wd_trav);
+                break;
+            }
+#endif
             const uint64_t tr = __builtin_amdgcn_ballot_w64(cur != THR_END);
             if (tr == 0) break;
             if ((uint32_t)__popcll(alive & ~tr) >= (uint32_t)A.shade_batch) break;
@@ -2050,6 +2144,169 @@ __global__ void gs_combine_kernel(const KParams* __restrict__ P) {
     }
 }
 
+// ------------------------------------------------ adaptive sampling in batch rounds
+// The reference's adaptive loop (camera.rs:135-165) runs a pixel's batches one after the
+// other, each batch's stop test over the running sums.  Per-lane that puts up to
+// max_samples + batch sequential samples of one pixel into one lane, and a frame ends on
+// its slowest pixels (an all-black pixel never converges, camera.rs:156).  In rounds, round
+// r renders batch r of every pixel still active, its samples split into work items like the
+// fixed-spp chunks, each sample's colour kept; the combine then folds a pixel's batch into
+// its sums in sample order and takes the stop test -- the same f64 operations in the same
+// order as the sequential loop, so every stop decision and every output is bit-identical.
+
+// Before round 0: padding slots get their zero output; every real packed pixel enters the
+// first active list (one atomic per wave; the order inside a wave is kept).
+__global__ void gs_round_init_kernel(const KParams* __restrict__ P) {
+    const uint32_t tile_px = (uint32_t)(P->tile_w * P->tile_h);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t cap = P->capacity;
+    const uint32_t span = (cap + 63u) & ~63u;  // whole waves take every iteration (ballots)
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < span; k += gridDim.x * blockDim.x) {
+        bool real = false;
+        if (k < cap) {
+            const uint32_t slot = k / tile_px, w = k % tile_px;
+            const uint32_t pos = (uint32_t)P->rank + slot * (uint32_t)P->world_size;
+            const uint32_t tile = P->order ? (uint32_t)P->order[pos] : pos;
+            if (tile != 0xFFFFFFFFu) {
+                const uint32_t pi = (tile % (uint32_t)P->tiles_x) * (uint32_t)P->tile_w + w % (uint32_t)P->tile_w;
+                const uint32_t pj = (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + w / (uint32_t)P->tile_w;
+                real = pi < (uint32_t)P->cam.image_width && pj < (uint32_t)P->cam.image_height;
+            }
+            if (!real) {
+                if (P->out) {
+                    float* o = P->out + (size_t)k * 3;
+                    o[0] = 0.0f;
+                    o[1] = 0.0f;
+                    o[2] = 0.0f;
+                }
+                if (P->out8) {
+                    uint8_t* o8 = P->out8 + (size_t)k * 3;
+                    o8[0] = 0;
+                    o8[1] = 0;
+                    o8[2] = 0;
+                }
+            }
+        }
+        const uint64_t m = __builtin_amdgcn_ballot_w64(real);
+        if (m == 0) continue;
+        const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&P->round_counts[0], (uint32_t)__popcll(m));
+        base = __shfl(base, (int)leader);
+        if (real) P->active_buf[0][base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = k;
+    }
+}
+
+// Before each (round, segment) launch: this launch's share of the round's active list, its
+// chunking (finer when few pixels are left, so the round's samples still spread over the
+// lanes), queue claim and cleared queue.
+__global__ void gs_round_params_kernel(KParams* __restrict__ P, uint32_t round, uint32_t seg, uint32_t seg_px,
+                                       int32_t chunk_req) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint32_t n_act = P->round_counts[round];
+    const uint32_t base = seg * seg_px;
+    const uint32_t n_seg = n_act > base ? min(seg_px, n_act - base) : 0u;
+    const uint32_t bs = P->ss.batch_size;
+    uint32_t csz;
+    if (chunk_req > 0) {
+        csz = min((uint32_t)chunk_req, bs);
+    } else {
+        csz = min(16u, bs);
+        while (csz > 1u && (uint64_t)n_seg * ((bs + csz - 1u) / csz) < 8ull * P->lanes) csz >>= 1;
+    }
+    const uint32_t cpp = (bs + csz - 1u) / csz;
+    P->chunk = csz;
+    P->cpp = cpp;
+    P->u_cpp = udiv_make(cpp);
+    P->n_items = n_seg * cpp;
+    P->fine_base = 0xFFFFFFFFu;  // no fine region
+    P->fine_px = P->capacity;
+    P->claim = max(1u, min(32u, P->n_items / max(1u, P->waves) / 8u));
+    P->claim_fine = P->claim;
+    P->round_base = round * bs;
+    P->seg_base = base;
+    P->seg_n = n_seg;
+    P->active = P->active_buf[round & 1u];
+    P->next_active = P->active_buf[(round & 1u) ^ 1u];
+    *P->queue = 0u;
+}
+
+// After each (round, segment) launch: per active pixel, its batch folded into the running
+// sums in sample order (camera.rs:142-146), then the stop test (:149-164) exactly as the
+// per-lane loop takes it; a stopped pixel's colour (:167) is written, the rest go on.
+__global__ void gs_round_combine_kernel(const KParams* __restrict__ P, uint32_t round) {
+    const uint32_t n = P->seg_n, bs = P->ss.batch_size, lane = threadIdx.x & 63u;
+    const uint32_t span = (n + 63u) & ~63u;
+    const double confidence_sq = P->ss.confidence * P->ss.confidence;
+    const double tolerance_sq = P->ss.tolerance * P->ss.tolerance;
+    // sample_count after this round's batch: 0.0 + bs + bs + ... (exact: integers < 2^53)
+    const double scount = (double)((uint64_t)(round + 1u) * bs);
+    for (uint32_t a = blockIdx.x * blockDim.x + threadIdx.x; a < span; a += gridDim.x * blockDim.x) {
+        bool go_on = false, stopped = false;
+        uint32_t item = 0;
+        if (a < n) {
+            item = P->active[P->seg_base + a];
+            double* ps = P->pstate + (size_t)item * 5;
+            double r = 0.0, g = 0.0, b = 0.0, lsum = 0.0, lsq = 0.0;
+            if (round) {
+                r = ps[0];
+                g = ps[1];
+                b = ps[2];
+                lsum = ps[3];
+                lsq = ps[4];
+            }
+            const double* smp = P->partial + (size_t)a * 3;
+            for (uint32_t j = 0; j < bs; j++, smp += (size_t)n * 3) {
+                const double cr = smp[0], cg = smp[1], cb = smp[2];
+                r += cr;
+                g += cg;
+                b += cb;
+                const double lum = 0.299 * cr + 0.587 * cg + 0.144 * cb;
+                lsum += lum;
+                lsq += lum * lum;
+            }
+            const double mean = lsum / scount;
+            const double variance_sq = 1.0 / (scount - 1.0) * (lsq - lsum * lsum / scount);
+            const double convergence_sq = confidence_sq * variance_sq / scount;
+            bool stop = convergence_sq < (mean * mean * tolerance_sq);
+            if (!stop) stop = (uint32_t)sat_u64(scount, 4294967295.0, 4294967295ull) > P->ss.max_samples;
+            if (stop) {
+                const double cr = r / scount, cg = g / scount, cb = b / scount;
+                if (P->out) {
+                    float* o = P->out + (size_t)item * 3;
+                    o[0] = (float)cr;
+                    o[1] = (float)cg;
+                    o[2] = (float)cb;
+                }
+                if (P->out8) {
+                    uint8_t* o8 = P->out8 + (size_t)item * 3;
+                    o8[0] = color_byte(cr);
+                    o8[1] = color_byte(cg);
+                    o8[2] = color_byte(cb);
+                }
+                stopped = true;
+            } else {
+                ps[0] = r;
+                ps[1] = g;
+                ps[2] = b;
+                ps[3] = lsum;
+                ps[4] = lsq;
+                go_on = true;
+            }
+        }
+        const uint64_t mg = __builtin_amdgcn_ballot_w64(go_on), ms = __builtin_amdgcn_ballot_w64(stopped);
+        if (mg != 0) {
+            const uint32_t leader = (uint32_t)__builtin_ctzll(mg);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&P->round_counts[round + 1u], (uint32_t)__popcll(mg));
+            base = __shfl(base, (int)leader);
+            if (go_on) P->next_active[base + (uint32_t)__popcll(mg & ((1ull << lane) - 1ull))] = item;
+        }
+        if (ms != 0 && P->counters && lane == (uint32_t)__builtin_ctzll(ms))
+            atomicAdd(&P->counters[C_PIX], (unsigned long long)__popcll(ms));
+    }
+}
+
 // =============================================================== host side
 static thread_local std::string tl_err;
 static int32_t g_shade_batch = 52;  // swept on MI355X C4 (chunked, uniform loop): 48 -> 3502, 52 -> 3535-3568, 56 -> 3506-3536 Msamples/s
@@ -2085,6 +2342,10 @@ static int64_t lds_mirror_budget() {
 static int32_t g_sample_chunk = -1;
 static int32_t g_placement = 1;  // 1: placement pilot at a scene's first launch; 0: the static estimate only
 static uint64_t g_partial_budget = 4ull << 30;  // auto chunks: at most 4 GiB of chunk sums (per launch slot)
+// Adaptive settings (more than one batch): 1 = batch rounds (gs_round_*_kernel), 0 = the
+// per-lane loop (one work item per pixel running every batch).  Bit-identical results.
+static int32_t g_adaptive_rounds = 1;
+static const uint64_t kMaxRounds = 1u << 16;  // more batches than this: the per-lane loop
 
 extern "C" void gs_set_last_error(const char* msg) { tl_err = msg ? msg : ""; }
 static gs_status fail(gs_status code, const std::string& msg) {
@@ -2109,6 +2370,9 @@ struct LaunchSlot {
     hipEvent_t done = nullptr;  // recorded after the slot's last launch
     hipStream_t stream = nullptr;  // the stream of the slot's last launch
     bool used = false;
+    // batch rounds (adaptive settings): round counts, the two active lists, the running sums
+    void* rbuf = nullptr;
+    size_t rbuf_bytes = 0;
 };
 static const int kLaunchSlots = 4;
 
@@ -2265,7 +2529,9 @@ static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* 
 
 // Host-side validation of everything the kernel indexes, so a malformed scene is an
 // error code, never a GPU fault.
-gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out) {
+// inst_reached (out): per instance, whether a leaf reachable from the root walks it (the scene
+// upload threads the BVHs under reached instances only).
+gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out, std::vector<uint8_t>* inst_reached) {
     auto bad = [](const std::string& m) { return fail(GS_ERR_ARG, "invalid flat scene: " + m); };
     auto unsup = [](const std::string& m) { return fail(GS_ERR_UNSUPPORTED, m); };
     if (!s.nodes && s.n_nodes) return bad("nodes");
@@ -2273,6 +2539,8 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
     // the kernel forms node / sphere byte offsets as u32 (ref << 6, ref << 5)
     if (s.n_nodes >= (1u << 26) || s.n_spheres >= (1u << 27)) return unsup("more than 2^26 BVH nodes or 2^27 spheres");
     if (s.n_materials == 0 || !s.materials) return bad("no materials");
+    if (!s.instances && s.n_instances) return bad("instances");
+    inst_reached->assign(s.n_instances, 0);
     auto prim_ok = [&](uint32_t r) {
         uint32_t k = r >> GS_REF_SHIFT, i = r & GS_REF_MASK;
         switch (k) {
@@ -2290,6 +2558,7 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
             uint32_t i = cur & GS_REF_MASK;
             if (i >= s.n_instances) return 1;
             if (++chain > GS_MAX_CHAIN) return 2;
+            (*inst_reached)[i] = 1;
             const gs_instance& in = s.instances[i];
             if (in.kind != GS_INST_TRANSLATE && in.kind != GS_INST_ROTATE_Y) return 1;
             cur = in.child;
@@ -2451,6 +2720,20 @@ bool encode_rgbe(const float* c, uint32_t* out) {
     return false;
 }
 
+// The device ref of a HittableList whose members are consecutive quads (DREF_QRUN: every
+// Quad::cube), or the ref itself (final_scene's box tests read the list
+// record and then each member's ref before each quad, a chain of dependent global loads).
+uint32_t qrun_ref(const gs_flat_scene& s, uint32_t ref) {
+    if (!GS_QRUN || (ref >> GS_REF_SHIFT) != GS_REF_LIST || (ref & GS_REF_MASK) >= s.n_lists) return ref;
+    const gs_list& l = s.lists[ref & GS_REF_MASK];
+    if (l.count == 0 || l.count >= 64 || (uint64_t)l.first + l.count > s.n_list_refs) return ref;
+    const uint32_t q0 = s.list_refs[l.first];
+    if ((q0 >> GS_REF_SHIFT) != GS_REF_QUAD || (q0 & GS_REF_MASK) + l.count > QRUN_FIRST_MASK) return ref;
+    for (uint32_t k = 0; k < l.count; k++)
+        if (s.list_refs[l.first + k] != q0 + k) return ref;
+    return (DREF_QRUN << GS_REF_SHIFT) | (q0 & GS_REF_MASK) | (l.count << QRUN_COUNT_SHIFT);
+}
+
 // Does the texture tree under `t` contain an image (=> sphere uv must be computed)?
 bool tex_needs_uv(const gs_flat_scene& s, uint32_t t, int depth = 0) {
     if (t >= s.n_textures || depth > 16) return false;
@@ -2490,6 +2773,12 @@ gs_status gs_set_placement(int32_t mode) {
     return GS_OK;
 }
 
+gs_status gs_set_adaptive_mode(int32_t mode) {
+    if (mode != 0 && mode != 1) return fail(GS_ERR_ARG, "adaptive mode is 0 (per-lane loop) or 1 (batch rounds)");
+    g_adaptive_rounds = mode;
+    return GS_OK;
+}
+
 gs_status gs_debug_set_partial_budget(uint64_t bytes) {
     g_partial_budget = bytes ? bytes : (4ull << 30);
     return GS_OK;
@@ -2500,7 +2789,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     *out = nullptr;
     uint32_t depth = 1;
     bool nested = false;
-    gs_status v = validate(*s, &depth, &nested);
+    std::vector<uint8_t> inst_reached;
+    gs_status v = validate(*s, &depth, &nested, &inst_reached);
     if (v != GS_OK) return v;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GS_ERR_NO_DEVICE, "no HIP device visible");
@@ -2515,8 +2805,16 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     std::vector<gs_instance> insts(s->instances, s->instances + s->n_instances);
     {
         std::unordered_map<uint32_t, uint32_t> start;  // node index -> first record
-        for (gs_instance& in : insts) {
+        for (size_t ii = 0; ii < insts.size(); ii++) {
+            gs_instance& in = insts[ii];
             if ((in.child >> GS_REF_SHIFT) != GS_REF_NODE) continue;
+            // Only instances a reachable leaf walks: validate() checked their trees (indices,
+            // depth, leaves); an unreachable one is never read by the kernel and may be
+            // malformed, so its node child is dropped, not walked.
+            if (!inst_reached[ii]) {
+                in.child = GS_REF_NONE;
+                continue;
+            }
             const uint32_t root = in.child & GS_REF_MASK;
             auto it = start.find(root);
             if (it == start.end()) {
@@ -2538,7 +2836,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                         if (n.right != GS_REF_NONE) work.push_back({n.right, false});
                         work.push_back({n.left, false});
                     } else {
-                        nodes.push_back(DNode{0, 0, 0, 0, 0, 0, idx + 1u, x, 1u, 0u});
+                        nodes.push_back(DNode{0, 0, 0, 0, 0, 0, idx + 1u, qrun_ref(*s, x), 1u, 0u});
                     }
                 }
                 const uint32_t end = (uint32_t)nodes.size();
@@ -2562,7 +2860,14 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             in.child = GS_MAKE_REF(GS_REF_NODE, it->second);
         }
         if (nodes.size() > GS_REF_MASK) return fail(GS_ERR_UNSUPPORTED, "more than 2^28 nested BVH records");
+        // the ends of instance chains that are lists of consecutive quads (Translate(RotateY(
+        // Quad::cube)): the Cornell boxes, main.rs:476-492)
+        for (size_t ii = 0; ii < insts.size(); ii++)
+            if (inst_reached[ii]) insts[ii].child = qrun_ref(*s, insts[ii].child);
     }
+    // media boundaries that are such lists (a chain's end is rewritten above)
+    std::vector<gs_medium> media(s->media, s->media + s->n_media);
+    for (gs_medium& m : media) m.boundary = qrun_ref(*s, m.boundary);
     // The threaded top-level tree (see THR_END): pre-order records of nodes and leaf
     // occurrences; raw links first, then split into node and leaf arrays.
     std::vector<DNode> thr;
@@ -2606,7 +2911,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                     rec.mxx = q.radius;
                 }
                 rec.left = idx + 1u;  // next
-                rec.right = x;        // the primitive's ABI ref
+                rec.right = qrun_ref(*s, x);  // the primitive's ref (a quad run: DREF_QRUN)
                 thr.push_back(rec);
                 thr_leaf.push_back(1);
             }
@@ -2771,7 +3076,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     size_t o_list = L.add(s->lists, s->n_lists * sizeof(gs_list));
     size_t o_lref = L.add(s->list_refs, s->n_list_refs * 4);
     size_t o_inst = L.add(insts.data(), insts.size() * sizeof(gs_instance));
-    size_t o_media = L.add(s->media, s->n_media * sizeof(gs_medium));
+    size_t o_media = L.add(media.data(), media.size() * sizeof(gs_medium));
     size_t o_perm = L.add(s->noise_perm, s->noise_perm ? s->n_noise_perm : 0);
     size_t o_mat = L.add(mats.data(), mats.size() * sizeof(DMaterial));
     size_t o_tex = L.add(s->textures, s->n_textures * sizeof(gs_texture));
@@ -2901,6 +3206,7 @@ gs_status gs_device_scene_destroy(gs_device_scene* ds) {
             (void)hipEventDestroy(sl.done);
         }
         if (sl.partial) (void)hipFree(sl.partial);
+        if (sl.rbuf) (void)hipFree(sl.rbuf);
     }
     if (ds->mem) (void)hipFree(ds->mem);
     delete ds;
@@ -3004,13 +3310,14 @@ struct VisitArgs {
 static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
                         const gs_partition* part, const gs_render_outputs* outs, gs_counters* d_counters, void* stream,
                         hipEvent_t k_begin, hipEvent_t k_end, const VisitArgs* va);
-static gs_status ensure_placement(gs_device_scene* ds, const gs_camera* cam, void* stream);
+static gs_status ensure_placement(gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
+                                  void* stream);
 
 gs_status gs_render_tiles_timed_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
                                       uint64_t seed, const gs_partition* part, const gs_render_outputs* outs,
                                       gs_counters* d_counters, void* stream, hipEvent_t k_begin, hipEvent_t k_end) {
     if (!ds || !cam) return fail(GS_ERR_ARG, "null argument");
-    gs_status e = ensure_placement(const_cast<gs_device_scene*>(ds), cam, stream);
+    gs_status e = ensure_placement(const_cast<gs_device_scene*>(ds), cam, ss, stream);
     if (e != GS_OK) return e;
     return launch(ds, cam, ss, seed, part, outs, d_counters, stream, k_begin, k_end, nullptr);
 }
@@ -3084,6 +3391,23 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     if ((uint64_t)fine_px * cpp + ((uint64_t)cap - fine_px) * fine_cpp >= 0xFFFFFFFFull)
         chunk = 0, cpp = 1, fine_px = (uint32_t)cap, fine_cpp = 1;
     if (!chunk) fine_px = (uint32_t)cap, fine_chunk = 1, fine_cpp = 1;
+    // Adaptive settings (more than one batch) in batch rounds: rounds = the most batches a
+    // pixel can run (the loop ends once sample_count > max_samples, camera.rs:162), in
+    // segments of at most seg_px active pixels whose per-sample colours fit the budget.
+    uint32_t n_rounds = 0, seg_px = 0, n_segs = 0;
+    if (g_adaptive_rounds && g_sample_chunk != 0 && ss->max_samples >= ss->batch_size && !outs->item_visits && !va) {
+        const uint64_t R = (uint64_t)ss->max_samples / ss->batch_size + 1u;
+        const uint64_t sp = std::min<uint64_t>((uint64_t)cap, g_partial_budget / ((uint64_t)ss->batch_size * 24u));
+        if (R <= kMaxRounds && sp >= 1 && sp * ss->batch_size < 0x7FFFFFFFull) {
+            n_rounds = (uint32_t)R;
+            seg_px = (uint32_t)sp;
+            n_segs = (uint32_t)(((uint64_t)cap + sp - 1) / sp);
+            chunk = 1;  // (the chunked lane layout; each round's chunking is set on the device)
+            cpp = 1;
+            fine_px = (uint32_t)cap, fine_chunk = 1, fine_cpp = 1;
+        }
+    }
+    kp.per_sample = n_rounds ? 1u : 0u;
     kp.chunk = chunk;
     kp.cpp = cpp;
     kp.fine_px = fine_px;
@@ -3160,13 +3484,15 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     a.lane_nd = lane_nd(chunked, ds->feat);
     const int per_cu = g_blocks_per_cu > 0 ? g_blocks_per_cu : lc.per_cu;
     int64_t blocks = (int64_t)cus * per_cu;
-    // no more waves than work: one lane per item at most
-    int64_t max_blocks = ((int64_t)kp.n_items + GS_BLOCK - 1) / GS_BLOCK;
+    // no more waves than work: one lane per item at most (a round's items: at most one per sample)
+    int64_t max_blocks = ((int64_t)(n_rounds ? (uint64_t)seg_px * ss->batch_size : kp.n_items) + GS_BLOCK - 1) / GS_BLOCK;
     if (blocks > max_blocks) blocks = max_blocks;
     if (blocks < 1) blocks = 1;
     // Items per queue claim: about 1/8 of a wave's share of the items, at most 32 (a wave
     // ends holding at most one partly used reserve), at least 1.
     const uint64_t waves = (uint64_t)blocks * (GS_BLOCK / 64);
+    kp.waves = (uint32_t)waves;
+    kp.lanes = (uint32_t)(blocks * GS_BLOCK);
     kp.claim = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, (uint64_t)kp.n_items / waves / 8));
 #ifndef GS_CLAIM_FINE
 #define GS_CLAIM_FINE 128  // MI355X C1 (1-2 sample items): 32 -> 6786, 128 -> 12397, 512 -> 12559; perlin 3169, 3221, 2670
@@ -3174,7 +3500,8 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     kp.claim_fine = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(GS_CLAIM_FINE, (uint64_t)kp.n_items / waves / 8));
     // The u32 queue counter runs past n_items by at most one claim per wave (each wave's
     // last, failed claim): it must not wrap.
-    if ((uint64_t)kp.n_items + (uint64_t)std::max(kp.claim, kp.claim_fine) * (waves + 1) >= 0xFFFFFFFFull)
+    if ((uint64_t)std::max<uint64_t>(kp.n_items, (uint64_t)seg_px * ss->batch_size) +
+            (uint64_t)std::max<uint32_t>(32, std::max(kp.claim, kp.claim_fine)) * (waves + 1) >= 0xFFFFFFFFull)
         return fail(GS_ERR_ARG, "too many work items for the 32-bit work queue");
 
     // This launch's slot.  A slot whose last launch ran on this very stream is reused first:
@@ -3182,7 +3509,8 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     // stream keeps one slot (and one chunk-sum buffer) however many launches it queues.
     // Otherwise a slot whose launch has finished, preferring one whose chunk sums are big
     // enough; otherwise the next in turn, behind a stream wait on its previous launch.
-    const size_t need_partial = chunk ? (size_t)kp.n_items * 3 * sizeof(double) : 0;
+    const size_t need_partial = n_rounds ? (size_t)seg_px * ss->batch_size * 3 * sizeof(double)
+                              : chunk ? (size_t)kp.n_items * 3 * sizeof(double) : 0;
     int pick = -1;
     for (int k = 0; k < kLaunchSlots && pick < 0; k++)
         if (mds->slots[k].used && mds->slots[k].stream == st) pick = k;
@@ -3214,12 +3542,56 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         }
         kp.partial = sl.partial;
     }
+    // batch rounds: [round counts][active list 0][active list 1][running sums], 256-B aligned
+    const size_t r_counts = ((size_t)(n_rounds + 2) * 4 + 255) & ~(size_t)255;
+    const size_t r_list = ((size_t)cap * 4 + 255) & ~(size_t)255;
+    if (n_rounds) {
+        const size_t need = r_counts + 2 * r_list + (size_t)cap * 5 * sizeof(double);
+        if (sl.rbuf_bytes < need) {
+            if (sl.used) HIPCHK(hipEventSynchronize(sl.done));
+            if (sl.rbuf) (void)hipFree(sl.rbuf);
+            sl.rbuf = nullptr;
+            sl.rbuf_bytes = 0;
+            if (hipMalloc(&sl.rbuf, need) != hipSuccess)
+                return fail(GS_ERR_OOM, "hipMalloc of " + std::to_string(need) + " bytes of batch-round state failed");
+            sl.rbuf_bytes = need;
+        }
+        uint8_t* rb = (uint8_t*)sl.rbuf;
+        kp.round_counts = (uint32_t*)rb;
+        kp.active_buf[0] = (uint32_t*)(rb + r_counts);
+        kp.active_buf[1] = (uint32_t*)(rb + r_counts + r_list);
+        kp.pstate = (double*)(rb + r_counts + 2 * r_list);
+    }
     kp.queue = sl.queue;
     a.P = sl.params;
     if (outs->item_visits) HIPCHK(hipMemsetAsync(outs->item_visits, 0, (size_t)cap * sizeof(uint32_t), st));
     hipLaunchKernelGGL(gs_params_kernel, dim3(1), dim3(64), 0, st, kp, sl.params);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(sl.queue, 0, 4, st));
+    if (n_rounds) {
+        // init (every real packed pixel active), then per round and segment: parameters,
+        // the megakernel, the combine; all on the stream, no host synchronisation (a segment
+        // or round with no active pixel left launches and exits at once)
+        KParams* dP = sl.params;
+        HIPCHK(hipMemsetAsync(kp.round_counts, 0, (size_t)(n_rounds + 1) * 4, st));
+        const unsigned g_init = (unsigned)std::min<int64_t>((cap + 255) / 256, 8192);
+        hipLaunchKernelGGL(gs_round_init_kernel, dim3(g_init), dim3(256), 0, st, (const KParams*)dP);
+        HIPCHK(hipGetLastError());
+        if (k_begin) HIPCHK(hipEventRecord(k_begin, st));
+        const unsigned g_comb = (unsigned)std::min<int64_t>((seg_px + 255) / 256, 8192);
+        for (uint32_t r = 0; r < n_rounds; r++)
+            for (uint32_t sg = 0; sg < n_segs; sg++) {
+                hipLaunchKernelGGL(gs_round_params_kernel, dim3(1), dim3(64), 0, st, dP, r, sg, seg_px, g_sample_chunk);
+                hipLaunchKernelGGL(kernel_for(lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
+                hipLaunchKernelGGL(gs_round_combine_kernel, dim3(g_comb), dim3(256), 0, st, (const KParams*)dP, r);
+            }
+        HIPCHK(hipGetLastError());
+        if (k_end) HIPCHK(hipEventRecord(k_end, st));
+        HIPCHK(hipEventRecord(sl.done, st));
+        sl.used = true;
+        sl.stream = st;
+        return GS_OK;
+    }
     if (k_begin) HIPCHK(hipEventRecord(k_begin, st));
     hipLaunchKernelGGL(kernel_for(va ? GS_FEAT_PILOT : lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
@@ -3245,8 +3617,19 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
 // bytes serves 99.6% and 96.0%, tools/visitmap.py).  Placement never changes a result
 // (links are explicit), and the pilot is deterministic, so every device of a multi-GPU
 // render places its copy identically.
-static gs_status run_pilot(gs_device_scene* ds, const gs_camera* cam, void* stream) {
-    const auto t0 = std::chrono::steady_clock::now();
+// The pilot in two halves, so a multi-GPU frame issues every device's pilot before it waits
+// for any (pilot_begin launches it on the stream, pilot_end waits, reads the counts back and
+// re-places the records).
+struct PilotRun {
+    std::chrono::steady_clock::time_point t0;
+    float* d_rgb = nullptr;
+    uint32_t* d_vis = nullptr;
+    hipStream_t st = nullptr;
+    bool launched = false;
+};
+
+// The pilot's camera: every k-th pixel of the launch's (~64 k pixels), 1 spp.
+static gs_camera pilot_camera(const gs_camera* cam) {
     const int64_t px = (int64_t)cam->image_width * cam->image_height;
     const int32_t k = std::max<int32_t>(1, (int32_t)std::sqrt((double)px / 65536.0));
     gs_camera pc = *cam;
@@ -3256,31 +3639,46 @@ static gs_status run_pilot(gs_device_scene* ds, const gs_camera* cam, void* stre
         pc.pixel_delta_u[a] = cam->pixel_delta_u[a] * (double)k;
         pc.pixel_delta_v[a] = cam->pixel_delta_v[a] * (double)k;
     }
+    return pc;
+}
+
+static gs_status pilot_begin(gs_device_scene* ds, const gs_camera* cam, void* stream, PilotRun& pr) {
+    pr.t0 = std::chrono::steady_clock::now();
+    const gs_camera pc = pilot_camera(cam);
     gs_partition part{0, 1, 64, 64, nullptr, 0, 0};
     const int64_t cap = gs_partition_capacity(&pc, &part);
     const uint32_t nn = ds->node_records, nl = ds->leaf_records;
-    float* d_rgb = nullptr;
-    uint32_t* d_vis = nullptr;
-    if (hipMalloc(&d_rgb, (size_t)cap * 12 + 16) != hipSuccess ||
-        hipMalloc(&d_vis, ((size_t)nn + nl) * 4 + 16) != hipSuccess) {
-        if (d_rgb) (void)hipFree(d_rgb);
+    if (hipMalloc(&pr.d_rgb, (size_t)cap * 12 + 16) != hipSuccess ||
+        hipMalloc(&pr.d_vis, ((size_t)nn + nl) * 4 + 16) != hipSuccess) {
+        if (pr.d_rgb) (void)hipFree(pr.d_rgb);
+        pr.d_rgb = nullptr;
         return fail(GS_ERR_OOM, "hipMalloc of the placement pilot's buffers failed");
     }
-    hipStream_t st = (hipStream_t)stream;
+    pr.st = (hipStream_t)stream;
     gs_sample_settings one{0.0, 0.0, 1, 0};  // one sample per pixel (camera.rs:158: max_samples < batch)
-    gs_render_outputs o{d_rgb, nullptr, nullptr};
-    VisitArgs va{d_vis, nn};
-    std::vector<uint32_t> vis((size_t)nn + nl);
-    hipError_t e = hipMemsetAsync(d_vis, 0, ((size_t)nn + nl) * 4, st);
+    gs_render_outputs o{pr.d_rgb, nullptr, nullptr};
+    VisitArgs va{pr.d_vis, nn};
+    hipError_t e = hipMemsetAsync(pr.d_vis, 0, ((size_t)nn + nl) * 4, pr.st);
     gs_status r = e == hipSuccess ? launch(ds, &pc, &one, 1, &part, &o, nullptr, stream, nullptr, nullptr, &va)
                                   : fail(GS_ERR_HIP, hipGetErrorString(e));
-    if (r == GS_OK) {
-        e = hipStreamSynchronize(st);
-        if (e == hipSuccess) e = hipMemcpy(vis.data(), d_vis, vis.size() * 4, hipMemcpyDeviceToHost);
+    pr.launched = r == GS_OK;
+    return r;
+}
+
+static gs_status pilot_end(gs_device_scene* ds, PilotRun& pr) {
+    const uint32_t nn = ds->node_records, nl = ds->leaf_records;
+    std::vector<uint32_t> vis((size_t)nn + nl);
+    gs_status r = GS_OK;
+    if (pr.launched) {
+        hipError_t e = hipStreamSynchronize(pr.st);
+        if (e == hipSuccess) e = hipMemcpy(vis.data(), pr.d_vis, vis.size() * 4, hipMemcpyDeviceToHost);
         if (e != hipSuccess) r = fail(GS_ERR_HIP, std::string("placement pilot: ") + hipGetErrorString(e));
     }
-    (void)hipFree(d_rgb);
-    (void)hipFree(d_vis);
+    if (pr.d_rgb) (void)hipFree(pr.d_rgb);
+    if (pr.d_vis) (void)hipFree(pr.d_vis);
+    pr.d_rgb = nullptr;
+    pr.d_vis = nullptr;
+    if (!pr.launched) return fail(GS_ERR_HIP, "placement pilot not launched");
     if (r != GS_OK) return r;
     const ThreadedTree& t = ds->tree;
     std::vector<uint64_t> counts(t.rec.size());
@@ -3302,24 +3700,68 @@ static gs_status run_pilot(gs_device_scene* ds, const gs_camera* cam, void* stre
         ds->pos = std::move(pl.pos);
         ds->lcfg[0].ready = ds->lcfg[1].ready = false;  // mirror prefixes changed
     }
-    ds->pilot_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return GS_OK;
-}
-
-static gs_status ensure_placement(gs_device_scene* ds, const gs_camera* cam, void* stream) {
-    if (ds->placement.load(std::memory_order_acquire) != 0) return GS_OK;
-    std::lock_guard<std::mutex> g(ds->place_mu);
-    if (ds->placement.load(std::memory_order_relaxed) != 0) return GS_OK;
-    const bool all_mirrored = ds->lds_nodes == ds->node_records && ds->lds_leaves == ds->leaf_records;
-    if (!g_placement || all_mirrored || cam->image_width <= 0 || cam->image_height <= 0) {
-        ds->placement.store(1, std::memory_order_release);
-        return GS_OK;
-    }
-    const gs_status r = run_pilot(ds, cam, stream);
-    if (r != GS_OK) return r;  // (tried again at the next launch)
+    ds->pilot_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - pr.t0).count();
     ds->tree = ThreadedTree{};  // not needed again
     ds->placement.store(2, std::memory_order_release);
     return GS_OK;
+}
+
+// Does this launch run the scene's pending pilot?  Not when placement is settled, or every
+// record is mirrored anyway (then it is settled as static), and not yet when the launch is
+// small next to the pilot: a pilot of ~64 k pixel samples before a launch of fewer than
+// 16 x as many samples costs more than a better mirror can save there (a one-shot 4-spp
+// frame of <= 64 k pixels would pay a full-frame pass, +25%), so it waits for a bigger one.
+static bool pilot_due(gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss) {
+    if (ds->placement.load(std::memory_order_acquire) != 0) return false;
+    const bool all_mirrored = ds->lds_nodes == ds->node_records && ds->lds_leaves == ds->leaf_records;
+    if (!g_placement || all_mirrored || !cam || cam->image_width <= 0 || cam->image_height <= 0) {
+        ds->placement.store(1, std::memory_order_release);
+        return false;
+    }
+    const gs_camera pc = pilot_camera(cam);
+    const uint64_t pilot_samples = (uint64_t)pc.image_width * (uint64_t)pc.image_height;
+    const uint64_t samples = (uint64_t)cam->image_width * (uint64_t)cam->image_height * (ss ? ss->batch_size : 1u);
+    return samples >= 16u * pilot_samples;
+}
+
+static gs_status ensure_placement(gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
+                                  void* stream) {
+    if (ds->placement.load(std::memory_order_acquire) != 0) return GS_OK;
+    std::lock_guard<std::mutex> g(ds->place_mu);
+    if (!pilot_due(ds, cam, ss)) return GS_OK;
+    PilotRun pr;
+    gs_status r = pilot_begin(ds, cam, stream, pr);
+    const gs_status r2 = pilot_end(ds, pr);  // (frees the buffers either way; tried again at the next launch)
+    return r != GS_OK ? r : r2;
+}
+
+// The frame context's first frame (and camera changes): every device's pending pilot is
+// launched before any is waited for, so N devices pilot concurrently (internal.hpp).
+gs_status gs_placement_prepare(gs_device_scene* const* scenes, const int* devices, void* const* streams, int n,
+                               const gs_camera* cam, const gs_sample_settings* ss) {
+    std::vector<std::unique_lock<std::mutex>> locks;
+    std::vector<PilotRun> runs(n);
+    std::vector<int> due(n, 0);
+    gs_status r = GS_OK;
+    for (int i = 0; i < n && r == GS_OK; i++) {
+        gs_device_scene* ds = scenes[i];
+        if (ds->placement.load(std::memory_order_acquire) != 0) continue;
+        locks.emplace_back(ds->place_mu);
+        if (!pilot_due(ds, cam, ss)) continue;
+        if (hipSetDevice(devices[i]) != hipSuccess) {
+            r = fail(GS_ERR_HIP, "hipSetDevice failed");
+            break;
+        }
+        due[i] = 1;
+        r = pilot_begin(ds, cam, streams[i], runs[i]);
+    }
+    for (int i = 0; i < n; i++) {
+        if (!due[i]) continue;
+        (void)hipSetDevice(devices[i]);
+        const gs_status e = pilot_end(scenes[i], runs[i]);
+        if (r == GS_OK) r = e;
+    }
+    return r;
 }
 
 extern "C" {
@@ -3351,7 +3793,7 @@ gs_status gs_plan_tiles(const gs_device_scene* ds, const gs_camera* cam, uint64_
     gs_status r = gs_render_tiles_ex_async(ds, cam, &one, seed, &all, &o, nullptr, nullptr);
     std::vector<uint32_t> vis((size_t)cap);
     if (r == GS_OK) {
-        hipError_t e = hipDeviceSynchronize();
+        hipError_t e = hipStreamSynchronize(nullptr);  // (the launch's stream: this device's alone)
         if (e == hipSuccess) e = hipMemcpy(vis.data(), d_vis, (size_t)cap * 4, hipMemcpyDeviceToHost);
         if (e != hipSuccess) r = fail(GS_ERR_HIP, hipGetErrorString(e));
     }
@@ -3398,7 +3840,7 @@ gs_status gs_debug_record_visits(const gs_device_scene* ds, const gs_camera* cam
                                  uint64_t seed, const gs_partition* part, float* d_packed_rgb, uint32_t* d_visits,
                                  void* stream) {
     if (!ds || !cam || !d_packed_rgb || !d_visits) return fail(GS_ERR_ARG, "null argument");
-    gs_status e = ensure_placement(const_cast<gs_device_scene*>(ds), cam, stream);
+    gs_status e = ensure_placement(const_cast<gs_device_scene*>(ds), cam, ss, stream);
     if (e != GS_OK) return e;
     HIPCHK(hipMemsetAsync(d_visits, 0, ((size_t)ds->node_records + ds->leaf_records) * 4, (hipStream_t)stream));
     gs_render_outputs o{d_packed_rgb, nullptr, nullptr};

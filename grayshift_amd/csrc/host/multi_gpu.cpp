@@ -161,7 +161,7 @@ struct gs_multi {
     bool comms_broken = false;      // a collective failed: the communicators were aborted
     int32_t tw = 64, th = 64;
     bool plan = false;
-    std::mutex mu;
+    mutable std::mutex mu;  // one frame at a time; guards every field below and comms_broken
     // tile partition of the last camera (plan or round-robin)
     bool part_ready = false;
     gs_camera part_cam{};
@@ -255,14 +255,25 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
     if (cam->image_width <= 0 || cam->image_height <= 0) return fail(GS_ERR_ARG, "bad image size");
     if (out && out->ppm_text && out->ppm_capacity < gs_ppm_max_bytes(cam->image_width, cam->image_height))
         return fail(GS_ERR_ARG, "ppm_capacity below gs_ppm_max_bytes");
-    if (comms_broken) return fail(GS_ERR_HIP, "the context's communicator was aborted after a failed collective");
     std::lock_guard<std::mutex> lock(mu);
+    if (comms_broken) return fail(GS_ERR_HIP, "the context's communicator was aborted after a failed collective");
     DeviceGuard guard;
     const auto t0 = std::chrono::steady_clock::now();
     const int n = (int)dev.size();
     double plan_ms = 0.0;
     gs_status s = partition(cam, seed, &plan_ms);
     if (s != GS_OK) return s;
+    {
+        // The scenes' placement pilots (first frame, render.hip run before the first launch):
+        // launched on every device before any is waited for, outside the timed render.
+        std::vector<gs_device_scene*> sc(n);
+        std::vector<void*> st(n);
+        for (int i = 0; i < n; i++) sc[i] = dev[i].scene, st[i] = dev[i].stream;
+        const auto tp = std::chrono::steady_clock::now();
+        s = gs_placement_prepare(sc.data(), ids.data(), st.data(), n, cam, ss);
+        if (s != GS_OK) return s;
+        plan_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
+    }
     const bool want_rgb = !out || out->rgb;
     const bool want8 = out && (out->rgb8 || out->ppm_text);
     const int64_t W = cam->image_width, H = cam->image_height;
@@ -464,6 +475,7 @@ gs_status gs_multi_render(gs_multi* m, const gs_camera* cam, const gs_sample_set
 
 gs_status gs_multi_frame(const gs_multi* m, const float** d_rgb, const uint8_t** d_rgb8, int32_t* device) {
     if (!m) return fail(GS_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lock(m->mu);  // (a frame being rendered replaces these)
     if (d_rgb) *d_rgb = m->have_rgb ? (const float*)m->frame.p : nullptr;
     if (d_rgb8) *d_rgb8 = m->have_rgb8 ? (const uint8_t*)m->frame8.p : nullptr;
     if (device) *device = m->dev[0].id;

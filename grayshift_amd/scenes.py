@@ -307,20 +307,28 @@ SCENES = {
     "final_scene": final_scene,
 }
 
-# BASELINE.json configs: (builder, kwargs, width, spp)
+# BASELINE.json configs: (builder, kwargs, width, spp).  spp None: the
+# scene's own adaptive SampleSettings, as main.rs renders every scene -- A1 the literal
+# default scene hdri() (main.rs:811-815: confidence 0.95, tolerance 0.05, batch 64, max 200)
+# at 1080p, A2 cornell_box (main.rs:497-501: 0.95, 0.5, 32, 1000) at 1024 x 1024.
 CONFIGS = {
     "C1": ("earth_hdr", {}, 400, 100),
     "C2": ("earth_hdr", {}, 1920, 256),
     "C3": ("cornell_box", {}, 1024, 1024),
     "C4": ("bouncing_spheres", {"grid": 50}, 1920, 512),
     "C5": ("mixed", {}, 3840, 4096),
+    "A1": ("hdri", {}, 1920, None),
+    "A2": ("cornell_box", {}, 1024, None),
 }
 
 
 def config(name, width=None, spp=None):
-    """A BASELINE config; width/spp overrides give the small parity-test versions.  A
-    reference scene's name (SCENES) gives that scene at fixed spp (default 400 px, 64 spp)."""
+    """A BASELINE config; width/spp overrides give the small parity-test versions (spp on an
+    adaptive config replaces its settings by fixed spp).  A reference scene's name (SCENES)
+    gives that scene at fixed spp (default 400 px, 64 spp)."""
     if name not in CONFIGS and name in SCENES:
         return SCENES[name](width=width or 400, settings=fixed_spp(spp or 64))
     scene, kw, w, s = CONFIGS[name]
+    if s is None and spp is None:
+        return SCENES[scene](width=width or w, **kw)  # the scene's own adaptive settings
     return SCENES[scene](width=width or w, settings=fixed_spp(spp or s), **kw)

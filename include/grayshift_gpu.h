@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 7
+#define GS_ABI_VERSION 8
 
 typedef int32_t gs_status;
 enum {
@@ -237,7 +237,13 @@ gs_status gs_set_node_steps(int32_t node_steps);
  * and the records are re-placed so the mirror holds the most-tested bytes (the pilot's
  * cost is reported as gs_scene_info.pilot_ms; results never depend on placement).
  * 0: keep the static estimate placed by gs_device_scene_create.  Applies to scenes
- * whose first launch comes after the call. */
+ * whose first launch comes after the call.
+ * Blocking (ABI 8 note): the launch that runs the pilot waits for it on the host (a
+ * stream synchronisation and a copy of the counts) before it issues its own kernels, so
+ * that one call of gs_render_tiles*_async is not asynchronous.  A launch of fewer than 16x
+ * the pilot's pixel samples (W*H*batch_size < 16 x ~64 k) leaves the pilot to a later,
+ * larger launch.  The frame context (gs_multi_render) runs the pilots of all its devices
+ * concurrently before its timed render. */
 gs_status gs_set_placement(int32_t mode);
 
 /* Diagnostic (ABI 7): one launch like gs_render_tiles_async that also counts, into the
@@ -247,6 +253,17 @@ gs_status gs_set_placement(int32_t mode);
 gs_status gs_debug_record_visits(const gs_device_scene* scene, const gs_camera* cam,
                                  const gs_sample_settings* ss, uint64_t seed, const gs_partition* part,
                                  float* d_packed_rgb, uint32_t* d_visits, void* stream);
+
+/* Adaptive settings (ABI 8) -- SampleSettings that run more than one batch
+ * (max_samples >= batch_size, camera.rs:135-165).  1 (default): batch rounds -- round r
+ * renders batch r of every pixel still active, its samples spread over the lanes like the
+ * fixed-spp chunks, each sample's colour kept; a combine pass then adds each pixel's batch
+ * into its running sums in sample order and takes the reference's stop test, so the
+ * result is bit-identical to the per-lane loop.  A launch then issues a few small kernels
+ * per round on its stream (no host synchronisation).  0: the per-lane loop (one work item
+ * per pixel running all of its batches; also used for more than 65536 possible batches,
+ * a sample chunk of 0, or the diagnostic per-pixel visit output). */
+gs_status gs_set_adaptive_mode(int32_t mode);
 
 /* Test hook: the auto sample-chunk rule's budget for chunk sums (default 4 GiB; 0
  * restores it).  A smaller budget makes renders take the chunk-doubling branch. */
@@ -287,7 +304,8 @@ gs_status gs_device_scene_info(const gs_device_scene* scene, gs_scene_info* out)
 typedef struct gs_stats {
     gs_counters counters;       /* work done, summed over devices (exact, = the oracle's) */
     double setup_ms;            /* host: scene uploads, communicator and tile plan of this call (one-shot
-                                   calls); gs_multi_render: the tile plan when it was (re)computed, else 0 */
+                                   calls); gs_multi_render: the tile plan when it was (re)computed, plus
+                                   the placement pilots of a scene's first frame (ABI 8), else 0 */
     double total_ms;            /* host: the whole call */
     double render_ms_max;       /* slowest device's render: parameter + megakernel + chunk-combine launches */
     double render_ms_min;       /* fastest device's */

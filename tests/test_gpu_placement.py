@@ -52,7 +52,8 @@ def test_placement_never_changes_the_frame(config, width, spp):
 
 def test_pilot_places_and_counts_the_frames_work():
     torch = pytest.importorskip("torch")
-    sc = scenes.config("C4", width=320, spp=4)
+    # (a launch of >= 16x the pilot's pixel samples: smaller ones leave the pilot pending)
+    sc = scenes.config("C4", width=160, spp=32)
     with _placement(0):
         r0 = g.Renderer(sc, 0, 1, 64)
         s_info, s_nodes, s_leaves, s_img = _visits(r0, torch)
@@ -84,3 +85,22 @@ def test_whole_tree_scenes_skip_the_pilot():
     assert info["lds_nodes"] == info["node_records"] and info["lds_leaves"] == info["leaf_records"]
     assert info["placement"] == 1 and info["pilot_ms"] == 0.0
     assert nodes.sum() > 0
+
+
+def test_small_launches_leave_the_pilot_pending():
+    """A launch of fewer than 16x the pilot's samples does not pay for a pilot:
+    the scene stays pending, and the next large launch runs it."""
+    torch = pytest.importorskip("torch")
+    small = scenes.config("C4", width=160, spp=4)
+    r = g.Renderer(small, 0, 1, 64)
+    dev = torch.device("cuda", 0)
+    packed = torch.zeros(r.capacity * 3, dtype=torch.float32, device=dev)
+    r.render_async(packed.data_ptr(), 0, 0, seed=3)
+    torch.cuda.synchronize()
+    assert r.scene_info()["placement"] == 0
+    big = scenes.config("C4", width=160, spp=32)
+    N.check(N.lib.gs_render_tiles_async(r.dev, C.byref(r.cam), C.byref(big.settings), 3, C.byref(r.part),
+                                        C.c_void_p(packed.data_ptr()), None, None))
+    torch.cuda.synchronize()
+    assert r.scene_info()["placement"] == 2
+    r.close()
