@@ -24,11 +24,12 @@ Rank 0 prints ONE JSON line with, beside the contract's fields:
   restated, oracle/) on a deterministic pixel subset, at the full config;
 * cpu_baseline — at N=1 the oracle's render time on that subset (median of 3, world and
   BVH build excluded), on this host's cores;
-* roofline — the kernel's binding ceiling, VALU issue: every VALU instruction class of the
-  PMC summary of this very code object (profiles/pmc/, keyed by the hash of the library's
-  gfx950 code objects) priced at its measured issue cycles (VALU_CYCLES), over the SIMDs'
-  cycles of this run's kernel time; the measured HBM fraction and the cache-served
-  algorithmic byte rate beside it.
+* roofline — the kernel's binding ceiling, VALU issue: the VALU busy cycles the PMC
+  counters of this very code object measured (profiles/pmc/, keyed by the hash of the
+  library's gfx950 code objects; 4 x (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2), below)
+  over the SIMDs' cycles of this run's kernel time, with the per-class pricing bracket
+  beside it (frac_lower / frac_upper); the measured HBM fraction and the cache-served
+  algorithmic byte rate beside those.
 """
 import argparse
 import json
@@ -63,6 +64,16 @@ SIMDS = 1024  # 256 CUs x 4 SIMDs
 # kernel -- more issue cycles than the SIMDs had -- so that bound is no longer reported.)
 VALU_CYCLES = {"ADD_F32": 2, "MUL_F32": 2, "FMA_F32": 2, "TRANS_F32": 8, "ADD_F64": 4, "MUL_F64": 4,
                "FMA_F64": 4, "TRANS_F64": 16, "INT32": 2, "INT64": 4, "CVT": 2, "OTHER": 2}
+# ... and the upper end of that bracket: every non-transcendental instruction at the VOP3 cost.
+VALU_CYCLES_UPPER = dict(VALU_CYCLES, ADD_F32=4, MUL_F32=4, FMA_F32=4, INT32=4, CVT=4, OTHER=4)
+# The point estimate (round 4, profiles/r04/valu_dual_issue_ubench.txt): on gfx950 every VALU
+# instruction holds its SIMD for SQ_ACTIVE_INST_VALU quad-cycles (1; 2 for v_sqrt_f32 class, 4
+# for f64 transcendentals), and two VOP1/VOP2 instructions of different waves can issue in one
+# quad-cycle, counted by SQ_ACTIVE_INST_VALU2.  On the microbenchmark 4 x (ACTIVE_INST_VALU -
+# ACTIVE_INST_VALU2) / instructions reproduces every measured cost: v_add_f32_e32 2.16 (measured
+# 2.20), v_fma_f32 with VGPRs 3.56 (3.65), v_fmac_f32_e32 3.65 (3.73), VOP3 / f64 4.0 (4.1-4.2),
+# v_sqrt_f32 8 (8.1), f64 rcp / sqrt 16 (16.1).  So the kernel's VALU busy cycles are measured,
+# not priced: busy = 4 x (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) summed over the SIMDs.
 PARITY_TOL = 1e-3  # north star: per-channel |delta| < 1e-3 vs the CPU path at a fixed seed
 
 
@@ -402,10 +413,17 @@ def roofline(a, c, world, kernel_ms, invalid):
     prof_s = pj["kernel_duration_ms_profiled"] / 1e3
     clock = k["GRBM_GUI_ACTIVE"] / 8.0 / prof_s  # effective shader clock of the profiled launch (Hz)
     cyc, mix = valu_cycles(k)
-    achieved = cyc / kernel_s  # VALU issue cycles per second, all SIMDs
+    cyc_hi, _ = valu_cycles(k, VALU_CYCLES_UPPER)
+    busy = None
+    if "SQ_ACTIVE_INST_VALU2" in k and "SQ_ACTIVE_INST_VALU" in k:
+        busy = 4.0 * (float(k["SQ_ACTIVE_INST_VALU"]) - float(k["SQ_ACTIVE_INST_VALU2"]))
     peak = SIMDS * clock
+    achieved = (busy if busy is not None else cyc) / kernel_s  # VALU issue cycles per second, all SIMDs
     wc = float(k.get("SQ_WAVE_CYCLES", 0.0)) or 1.0
     out.update({"achieved": round(achieved / 1e9, 2), "peak": round(peak / 1e9, 2), "frac": round(achieved / peak, 4),
+                "frac_method": ("measured: 4 x (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) busy quad-cycles"
+                                if busy is not None else "priced: VALU_CYCLES per PMC class"),
+                "frac_lower": round(cyc / kernel_s / peak, 4), "frac_upper": round(cyc_hi / kernel_s / peak, 4),
                 "traffic": pj["hbm_bytes_per_launch"],
                 "hbm_frac": round(pj["hbm_bytes_per_launch"] / kernel_s / 1e9 / HBM_PEAK_GBS, 5),
                 "effective_clock_ghz": round(clock / 1e9, 3),

@@ -67,6 +67,11 @@ using namespace gsd;
 #define GS_QRUN 0
 #endif
 #define DREF_QRUN 9u
+// The nested trees' records (BVHs under instances) mirrored in LDS after the quads, placed
+// shallowest first (0: read from global memory only)
+#ifndef GS_NESTED_LDS
+#define GS_NESTED_LDS 0
+#endif
 #define QRUN_COUNT_SHIFT 22u
 #define QRUN_FIRST_MASK ((1u << QRUN_COUNT_SHIFT) - 1u)
 #define GS_NESTED_STACK 32  // max depth of a BVH under a Translate/RotateY chain (validation bound: the walk is stackless)
@@ -218,6 +223,8 @@ struct KArgs {
     uint32_t lds_nodes;  // node records [0, lds_nodes) are mirrored in each block's LDS,
     uint32_t lds_leaves; // then leaf records [0, lds_leaves)
     uint32_t lds_quads;  // then quad records [0, lds_quads)
+    uint32_t lds_nrecs;  // then the nested trees' records [0, lds_nrecs) (GS_NESTED_LDS)
+    const TNode* nrecs;  // (the mirror's source)
     uint32_t lane_nd;    // f64 lane-state fields in LDS: lane_nd(chunked)
 };
 
@@ -358,6 +365,9 @@ struct QuadSrc {
     const uint8_t* lds;
     const TQuad* g;
     uint32_t n_lds;
+    // the nested trees' records mirrored in LDS: [0, n_nlds) at nlds (GS_NESTED_LDS)
+    const uint8_t* nlds;
+    uint32_t n_nlds;
 };
 
 // Scene-record loads of the leaf tests, field by field through a pointer of an explicit
@@ -519,16 +529,36 @@ __device__ __forceinline__ uint32_t walk_chain(const DevScene& sc, uint32_t cur,
 // A device-side QRUN ref (DREF_QRUN, set at upload: render.hip qrun_ref) is a list whose
 // members are the quads [first, first + count) in order (every Quad::cube, quad.rs:54-80),
 // so neither the list record nor its member refs are read: the same quads in the same order.
-template <bool UNI>
+// QR: this call site may meet QRUN refs (top-level and nested leaves, instance chains that
+// end in a list; not medium boundaries, which the host leaves as plain lists).
+template <bool UNI, bool QR = true>
 __device__ __forceinline__ void shape_test(const DevScene& sc, const QuadSrc& qs, uint32_t cur, const Ray& r,
                                            double tmin, double closest, uint32_t inst_ref, LeafHit& res,
                                            unsigned long long* cnt) {
+#if GS_QRUN
+    const uint32_t kind = cur >> GS_REF_SHIFT;
+    if (kind == GS_REF_LIST || (QR && kind == DREF_QRUN)) {
+        atomicAdd(&cnt[C_LIST], 1ull);
+        const bool direct = QR && kind == DREF_QRUN;
+        gs_list l;
+        if (direct) {
+            l.first = cur & QRUN_FIRST_MASK;
+            l.count = (cur & GS_REF_MASK) >> QRUN_COUNT_SHIFT;
+        } else {
+            l = ld_list<UNI>(sc.lists + (cur & GS_REF_MASK));
+        }
+#pragma unroll 1
+        for (uint32_t k = 0; k < l.count; k++)
+            prim_test<UNI>(sc, qs, direct ? GS_MAKE_REF(GS_REF_QUAD, l.first + k) : ld_u32<UNI>(sc.list_refs + l.first + k),
+                           r, tmin, res.t, inst_ref, res, cnt);
+#else
     if ((cur >> GS_REF_SHIFT) == GS_REF_LIST) {
         atomicAdd(&cnt[C_LIST], 1ull);
         const gs_list l = ld_list<UNI>(sc.lists + (cur & GS_REF_MASK));
 #pragma unroll 1
         for (uint32_t k = 0; k < l.count; k++)
             prim_test<UNI>(sc, qs, ld_u32<UNI>(sc.list_refs + l.first + k), r, tmin, res.t, inst_ref, res, cnt);
+#endif
     } else {
         prim_test<UNI>(sc, qs, cur, r, tmin, closest, inst_ref, res, cnt);
     }
@@ -553,14 +583,14 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
     b1.t = DMAX;
     Ray rb = r;
     const uint32_t shape = walk_chain<UNI>(sc, md.boundary, rb, cnt);
-    shape_test<UNI>(sc, qs, shape, rb, -DMAX, DMAX, GS_REF_NONE, b1, cnt);
+    shape_test<UNI, false>(sc, qs, shape, rb, -DMAX, DMAX, GS_REF_NONE, b1, cnt);
     if (!b1.hit) return;
     LeafHit b2;
     b2.hit = false;
     b2.t = DMAX;
     rb = r;
     walk_chain<UNI>(sc, md.boundary, rb, cnt);  // the second boundary.hit call walks the chain again
-    shape_test<UNI>(sc, qs, shape, rb, b1.t + 0.0001, DMAX, GS_REF_NONE, b2, cnt);
+    shape_test<UNI, false>(sc, qs, shape, rb, b1.t + 0.0001, DMAX, GS_REF_NONE, b2, cnt);
     if (!b2.hit) return;
     double t1 = b1.t, t2 = b2.t;
     if (t1 < tmin) t1 = tmin;
@@ -604,8 +634,16 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
     uint32_t cur = root;
 #pragma unroll 1
     while (cur != THR_END) {
-        const u32x4* q = sp<false>(reinterpret_cast<const u32x4*>(sc.nrecs + cur));
-        const u32x4 a = q[0], b = q[1];
+        u32x4 a, b;
+        // (a scalar branch to the LDS reads when every active lane's record is mirrored)
+        if (__builtin_amdgcn_ballot_w64(cur >= qs.n_nlds) == 0) {
+            a = *(lds_u32x4*)(qs.nlds + cur * 32u);
+            b = *(lds_u32x4*)(qs.nlds + cur * 32u + 16u);
+        } else {
+            const u32x4* q = sp<false>(reinterpret_cast<const u32x4*>(sc.nrecs + cur));
+            a = q[0];
+            b = q[1];
+        }
         if (b.z & NREC_LEAF) {  // a leaf occurrence: test it, then the next record
             shape_test<false>(sc, qs, b.w, r, tmin, closest, inst_ref, res, cnt);
             if (res.hit) {  // res.t only ever shrinks
@@ -1190,10 +1228,16 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         src = reinterpret_cast<const uint4*>(A.tquads);
         dst = reinterpret_cast<uint4*>(s_quads);
         for (uint32_t k = threadIdx.x; k < A.lds_quads * 8u; k += GS_BLOCK) dst[GS_QUAD_SWZ ? k ^ ((k >> 3) & 7u) : k] = src[k];
+        if constexpr ((FEAT & GS_FEAT_NESTED) != 0) {
+            src = reinterpret_cast<const uint4*>(A.nrecs);
+            dst = reinterpret_cast<uint4*>(s_quads + (size_t)A.lds_quads * sizeof(TQuad));
+            for (uint32_t k = threadIdx.x; k < A.lds_nrecs * 2u; k += GS_BLOCK) dst[k] = src[k];
+        }
     }
-    const QuadSrc qs{s_quads, A.tquads, A.lds_quads};
+    uint8_t* s_nrecs = s_quads + (size_t)A.lds_quads * sizeof(TQuad);
+    const QuadSrc qs{s_quads, A.tquads, A.lds_quads, s_nrecs, A.lds_nrecs};
     // Per-lane pixel / path state after the mirror: [L_ND][GS_BLOCK] f64, [L_NI][GS_BLOCK] u32.
-    double* s_d = (double*)(s_quads + (size_t)A.lds_quads * sizeof(TQuad));
+    double* s_d = (double*)(s_nrecs + (size_t)A.lds_nrecs * sizeof(TNode));
     uint32_t* s_i = (uint32_t*)(s_d + A.lane_nd * GS_BLOCK);
     unsigned long long* s_cnt = (unsigned long long*)(s_i + lane_ni(FEAT) * GS_BLOCK);
 #ifdef GS_STAMPS
@@ -1254,6 +1298,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     bool fresh = false;
     // hot counters kept in registers, flushed per pixel
     uint32_t c_nodes = 0, c_sph = 0;  // (per lane: one VALU add beat a 64-bit SALU wave count)
+    // GS_SALU_COUNT: node visits counted per wave on the scalar unit (popcount of the step's
+    // lane mask), not per lane on the VALU -- the kernel's VALU is ~88% busy.
+    // Launches that need per-pixel counts (item_visits) run the pilot's instantiation.
+#ifndef GS_SALU_COUNT
+#define GS_SALU_COUNT 0
+#endif
+    constexpr bool kSaluCount = GS_SALU_COUNT && (FEAT & GS_FEAT_VISITS) == 0;
+    uint64_t w_nodes = 0;
 
     auto begin_ray = [&]() {
         // AABB::hit's `1.0 / ray.direction[axis]` (AABB.rs:64), hoisted per ray (same value)
@@ -1306,7 +1358,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     // a stationary-sphere test: a lane count (flushed with c_nodes), or in t_in_lds kernels
     // a wave-aggregated LDS atomic, as prim_test counts the other kinds (no register kept)
     auto count_sph = [&]() __attribute__((always_inline)) {
-        if constexpr (kTLds) atomicAdd(&s_cnt[C_SPH], 1ull);
+        if constexpr (kTLds || kSaluCount) atomicAdd(&s_cnt[C_SPH], 1ull);
         else c_sph++;
     };
     auto end_chunk = [&]() {
@@ -1672,6 +1724,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     d_wlanes += (uint64_t)__popcll(act);
                 }
 #endif
+                if constexpr (kSaluCount) w_nodes += (uint64_t)__popcll(__builtin_amdgcn_ballot_w64(LDSP ? cur < lim : cur < THR_END));
                 if (__builtin_expect(LDSP ? cur < lim : cur < THR_END, 1)) {
                     // One 32-B record (2 x 16 B; from LDS, offset = cur, or off the SGPR
                     // base), the box test, and the next record: the hit link or the miss link.
@@ -1682,8 +1735,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     } else {
                         load_tnode_w<(FEAT & GS_FEAT_LDSTREE) != 0>(s_nodes, A.tnodes, cur, A.lds_nodes << 5, ra, rb);
                     }
-                    c_nodes++;
-                    if constexpr ((FEAT & GS_FEAT_VISITS) != 0) count_visit(P->visits, cur >> 5);
+                    if constexpr (!kSaluCount) c_nodes++;
+                    if constexpr ((FEAT & GS_FEAT_VISITS) != 0) {
+                        if (P->visits) count_visit(P->visits, cur >> 5);
+                    }
                     const uint32_t me = cur;  // this record
                     if constexpr (FAST) {
                         // the certified decision picks the link at once; lanes f32 cannot
@@ -1787,7 +1842,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                 }
                 if (take_leaf) {
-                if constexpr ((FEAT & GS_FEAT_VISITS) != 0) count_visit(P->visits, P->visit_leaf_base + (cur & ~THR_LEAF));
+                if constexpr ((FEAT & GS_FEAT_VISITS) != 0) {
+                    if (P->visits) count_visit(P->visits, P->visit_leaf_base + (cur & ~THR_LEAF));
+                }
 #ifdef GS_STAMPS
                 {  // counted by the pass's first active lane (summed over lanes at the end)
                     const uint64_t act = __builtin_amdgcn_ballot_w64(true);
@@ -1841,8 +1898,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         hit_ref = ref;
                     }
                     if (two) {
-                        if constexpr ((FEAT & GS_FEAT_VISITS) != 0)
-                            count_visit(P->visits, P->visit_leaf_base + (next & ~THR_LEAF));
+                        if constexpr ((FEAT & GS_FEAT_VISITS) != 0) {
+                            if (P->visits) count_visit(P->visits, P->visit_leaf_base + (next & ~THR_LEAF));
+                        }
                         if (sphere_take(q2, tmin, closest, t)) {
                             closest = t;
                             hit_ref = ref2;
@@ -1850,7 +1908,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         next = next2;
                     }
                     closest32 = (float)closest;
-                    c_sph += 1u + (uint32_t)two;
+                    if constexpr (kSaluCount) {  // (uniform increments: one LDS add per wave each)
+                        atomicAdd(&s_cnt[C_SPH], 1ull);
+                        if (two) atomicAdd(&s_cnt[C_SPH], 1ull);
+                    } else {
+                        c_sph += 1u + (uint32_t)two;
+                    }
                     GS_MARK("sphere_end");
                 } else if ((FEAT & GS_FEAT_SPHLEAF) != 0 || (ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {
                     sphere_leaf();
@@ -1891,8 +1954,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     load_tleaf<(FEAT & GS_FEAT_LDSTREE) != 0>(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr,
                                                          next, ref);
                     if ((FEAT & GS_FEAT_SPHLEAF) == 0 && (ref >> GS_REF_SHIFT) != GS_REF_SPHERE) break;
-                    if constexpr ((FEAT & GS_FEAT_VISITS) != 0)
-                        count_visit(P->visits, P->visit_leaf_base + (cur & ~THR_LEAF));
+                    if constexpr ((FEAT & GS_FEAT_VISITS) != 0) {
+                        if (P->visits) count_visit(P->visits, P->visit_leaf_base + (cur & ~THR_LEAF));
+                    }
                     count_sph();
                     double t;
                     if (sphere_accept(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
@@ -2076,6 +2140,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #undef GS_TP
 
     // flush counters: LDS -> global, one atomic per counter per block
+    if constexpr (kSaluCount) {
+        if (lane == 0) atomicAdd(&s_cnt[C_NODES], (unsigned long long)w_nodes);
+    }
     atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
     atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
     __syncthreads();
@@ -2401,6 +2468,8 @@ struct gs_device_scene {
     const TQuad* tquads = nullptr;  // every quad's traversal record, gs_quad order
     uint32_t thr_root = THR_END;
     uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0;  // mirrored prefixes (per block)
+    uint32_t n_nrecs = 0, lds_nrecs = 0;  // nested trees' records, and the mirrored prefix of them
+    const TNode* nrecs = nullptr;
     int32_t node_steps = GS_NODE_STEPS;      // node steps per node pass (from the tree's shape)
     int32_t leaf_batch = 12;                 // lanes at a leaf before a leaf pass (scene's choice)
     uint32_t node_records = 0, leaf_records = 0;
@@ -2413,7 +2482,7 @@ struct gs_device_scene {
     // instantiation (feat minus GS_FEAT_LDSTREE when the mirror is a strict prefix), blocks/CU.
     struct LaunchCfg {
         bool ready = false;
-        uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0;
+        uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_nrecs = 0;
         size_t lds = 0;
         int feat = 0, per_cu = 0;
     } lcfg[2];
@@ -2450,7 +2519,7 @@ struct Placed {
     std::vector<TBox> tboxes;
     std::vector<TLeaf> tleaves;
     std::vector<uint32_t> pos;  // tree record -> its position in tnodes / tleaves
-    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, root = THR_END;
+    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_nrecs = 0, root = THR_END;
 };
 #ifndef GS_LDS_LEAVES
 #define GS_LDS_LEAVES 1  // 0: mirror node records only
@@ -2462,7 +2531,7 @@ struct Placed {
 // orders the unvisited and serves when there is no pilot.  Records outside the mirror
 // stay in pre-order.
 static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* visits, uint32_t n_quads,
-                            int64_t budget) {
+                            int64_t budget, uint32_t n_nrecs) {
     const uint32_t n = (uint32_t)t.rec.size();
     Placed out;
     std::vector<uint32_t> order(n), pos(n);
@@ -2496,6 +2565,11 @@ static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* 
         top[r] = 1;
         (t.leaf[r] ? out.lds_leaves : out.lds_nodes)++;
     }
+    // then the nested trees' records (shallowest first: they are placed by depth), then quads
+    out.lds_nrecs = GS_NESTED_LDS ? (uint32_t)std::min<int64_t>(n_nrecs, std::max<int64_t>(0, budget - used) /
+                                                                        (int64_t)sizeof(TNode))
+                                  : 0u;
+    used += (int64_t)out.lds_nrecs * (int64_t)sizeof(TNode);
     out.lds_quads = (uint32_t)std::min<int64_t>(n_quads, std::max<int64_t>(0, budget - used) / (int64_t)sizeof(TQuad));
     // The mirrored records take their positions in rank order, so a launch that must
     // shrink the prefixes (a larger lane state, gs_render_tiles_timed_async) drops the
@@ -2552,13 +2626,14 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
         }
     };
     // Walks a Translate/RotateY chain: 0 ok, 1 bad, 2 unsupported (deeper than GS_MAX_CHAIN).
-    auto chain_ok = [&](uint32_t& cur) -> int {
+    // mark: 1 a leaf's chain, 2 a medium boundary's (kept: a chain reached both ways is 2)
+    auto chain_ok = [&](uint32_t& cur, uint8_t mark = 1) -> int {
         int chain = 0;
         while ((cur >> GS_REF_SHIFT) == GS_REF_INSTANCE) {
             uint32_t i = cur & GS_REF_MASK;
             if (i >= s.n_instances) return 1;
             if (++chain > GS_MAX_CHAIN) return 2;
-            (*inst_reached)[i] = 1;
+            (*inst_reached)[i] = std::max((*inst_reached)[i], mark);
             const gs_instance& in = s.instances[i];
             if (in.kind != GS_INST_TRANSLATE && in.kind != GS_INST_ROTATE_Y) return 1;
             cur = in.child;
@@ -2616,7 +2691,7 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
             if (i >= s.n_media || !s.media) return 1;
             if (s.media[i].material >= s.n_materials) return 1;
             uint32_t b = s.media[i].boundary;
-            e = chain_ok(b);
+            e = chain_ok(b, 2);
             if (e) return e;
             return shape_ok(b);
         }
@@ -2805,6 +2880,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     std::vector<gs_instance> insts(s->instances, s->instances + s->n_instances);
     {
         std::unordered_map<uint32_t, uint32_t> start;  // node index -> first record
+        std::vector<uint32_t> ndepth;                  // each record's depth in its tree
         for (size_t ii = 0; ii < insts.size(); ii++) {
             gs_instance& in = insts[ii];
             if ((in.child >> GS_REF_SHIFT) != GS_REF_NODE) continue;
@@ -2819,24 +2895,30 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             auto it = start.find(root);
             if (it == start.end()) {
                 const uint32_t first = (uint32_t)nodes.size();
-                std::vector<std::pair<uint32_t, bool>> work{{in.child, false}};
+                struct Work {
+                    uint32_t x;
+                    bool close;
+                    uint32_t depth;
+                };
+                std::vector<Work> work{{in.child, false, 0u}};
                 while (!work.empty()) {
-                    auto [x, close] = work.back();
+                    const Work w = work.back();
                     work.pop_back();
-                    if (close) {
-                        nodes[x].right = (uint32_t)nodes.size();
+                    if (w.close) {
+                        nodes[w.x].right = (uint32_t)nodes.size();
                         continue;
                     }
                     const uint32_t idx = (uint32_t)nodes.size();
-                    if ((x >> GS_REF_SHIFT) == GS_REF_NODE) {
-                        const gs_node& n = s->nodes[x & GS_REF_MASK];
+                    ndepth.push_back(w.depth);
+                    if ((w.x >> GS_REF_SHIFT) == GS_REF_NODE) {
+                        const gs_node& n = s->nodes[w.x & GS_REF_MASK];
                         nodes.push_back(DNode{n.min[0], n.min[1], n.min[2], n.max[0], n.max[1], n.max[2], idx + 1u, 0u,
                                               0u, 0u});
-                        work.push_back({idx, true});
-                        if (n.right != GS_REF_NONE) work.push_back({n.right, false});
-                        work.push_back({n.left, false});
+                        work.push_back({idx, true, 0u});
+                        if (n.right != GS_REF_NONE) work.push_back({n.right, false, w.depth + 1u});
+                        work.push_back({n.left, false, w.depth + 1u});
                     } else {
-                        nodes.push_back(DNode{0, 0, 0, 0, 0, 0, idx + 1u, qrun_ref(*s, x), 1u, 0u});
+                        nodes.push_back(DNode{0, 0, 0, 0, 0, 0, idx + 1u, qrun_ref(*s, w.x), 1u, 0u});
                     }
                 }
                 const uint32_t end = (uint32_t)nodes.size();
@@ -2844,30 +2926,49 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                     if (nodes[k].left == end) nodes[k].left = THR_END;
                     if (!nodes[k].pad0 && nodes[k].right == end) nodes[k].right = THR_END;
                 }
-                for (uint32_t k = first; k < end; k++) {  // the f32 records (nested_bvh)
-                    const DNode& n = nodes[k];
-                    if (n.pad0) {
-                        nrecs.push_back(TNode{0, 0, 0, 0, 0, 0, NREC_LEAF | n.left, n.right});
-                    } else {
-                        nrecs.push_back(TNode{(float)n.mnx, (float)n.mny, (float)n.mxx, (float)n.mxy, (float)n.mnz,
-                                              (float)n.mxz, n.left, n.right});
-                        for (double v : {n.mnx, n.mny, n.mnz, n.mxx, n.mxy, n.mxz})
-                            if (!(std::fabs(v) <= 1e15)) nested_cert = false;
-                    }
-                }
                 it = start.emplace(root, first).first;
             }
             in.child = GS_MAKE_REF(GS_REF_NODE, it->second);
         }
+        // Placement of the nested records (GS_NESTED_LDS): shallowest first, so the LDS mirror's
+        // prefix holds every tree's top levels, the records a walk tests most (links are
+        // explicit, so order never changes a walk).
+        if (GS_NESTED_LDS && !nodes.empty()) {
+            const uint32_t n = (uint32_t)nodes.size();
+            std::vector<uint32_t> order(n), npos(n);
+            for (uint32_t k = 0; k < n; k++) order[k] = k;
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return ndepth[a] < ndepth[b]; });
+            for (uint32_t k = 0; k < n; k++) npos[order[k]] = k;
+            auto link = [&](uint32_t l) { return l == THR_END ? THR_END : npos[l]; };
+            std::vector<DNode> placed(n);
+            for (uint32_t k = 0; k < n; k++) {
+                DNode d = nodes[k];
+                d.left = link(d.left);                // hit link / next
+                if (!d.pad0) d.right = link(d.right);  // miss link (a leaf's right is its ref)
+                placed[npos[k]] = d;
+            }
+            nodes.swap(placed);
+            for (gs_instance& in : insts)
+                if ((in.child >> GS_REF_SHIFT) == GS_REF_NODE) in.child = GS_MAKE_REF(GS_REF_NODE, npos[in.child & GS_REF_MASK]);
+        }
+        for (const DNode& n : nodes) {  // the f32 records (nested_bvh), index-aligned with nodes
+            if (n.pad0) {
+                nrecs.push_back(TNode{0, 0, 0, 0, 0, 0, NREC_LEAF | n.left, n.right});
+            } else {
+                nrecs.push_back(TNode{(float)n.mnx, (float)n.mny, (float)n.mxx, (float)n.mxy, (float)n.mnz, (float)n.mxz,
+                                      n.left, n.right});
+                for (double v : {n.mnx, n.mny, n.mnz, n.mxx, n.mxy, n.mxz})
+                    if (!(std::fabs(v) <= 1e15)) nested_cert = false;
+            }
+        }
         if (nodes.size() > GS_REF_MASK) return fail(GS_ERR_UNSUPPORTED, "more than 2^28 nested BVH records");
         // the ends of instance chains that are lists of consecutive quads (Translate(RotateY(
         // Quad::cube)): the Cornell boxes, main.rs:476-492)
+        // (not the chains of medium boundaries: medium_test reads plain lists, inst_reached 2)
         for (size_t ii = 0; ii < insts.size(); ii++)
-            if (inst_reached[ii]) insts[ii].child = qrun_ref(*s, insts[ii].child);
+            if (inst_reached[ii] == 1) insts[ii].child = qrun_ref(*s, insts[ii].child);
     }
-    // media boundaries that are such lists (a chain's end is rewritten above)
     std::vector<gs_medium> media(s->media, s->media + s->n_media);
-    for (gs_medium& m : media) m.boundary = qrun_ref(*s, m.boundary);
     // The threaded top-level tree (see THR_END): pre-order records of nodes and leaf
     // occurrences; raw links first, then split into node and leaf arrays.
     std::vector<DNode> thr;
@@ -2875,7 +2976,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     std::vector<TNode> tnodes;
     std::vector<TBox> tboxes;
     std::vector<TLeaf> tleaves;
-    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, thr_root_tagged = THR_END;
+    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_nrecs = 0, thr_root_tagged = THR_END;
     ThreadedTree tree_keep;  // kept by the scene: re-placed after a launch's pilot (place_records)
     std::vector<uint32_t> placed_pos;
     double nodes_per_leaf = 0.0, other_leaf_frac = 0.0;
@@ -2967,13 +3068,14 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         }
         tree_keep = ThreadedTree{thr, thr_leaf, std::move(depth), std::move(score)};
         const Placed pl = place_records(tree_keep, nullptr, s->n_quads,
-                                        g_lds_mirror < 0 ? lds_mirror_budget() : g_lds_mirror);
+                                        g_lds_mirror < 0 ? lds_mirror_budget() : g_lds_mirror, (uint32_t)nrecs.size());
         tnodes = pl.tnodes;
         tboxes = pl.tboxes;
         tleaves = pl.tleaves;
         lds_nodes = pl.lds_nodes;
         lds_leaves = pl.lds_leaves;
         lds_quads = pl.lds_quads;
+        lds_nrecs = pl.lds_nrecs;
         thr_root_tagged = pl.root;
         placed_pos = pl.pos;
         // Leaf runs pay when at least a quarter of the leaf records are the first of two
@@ -3140,6 +3242,9 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ds->lds_nodes = lds_nodes;
     ds->lds_leaves = lds_leaves;
     ds->lds_quads = lds_quads;
+    ds->lds_nrecs = lds_nrecs;
+    ds->n_nrecs = (uint32_t)nrecs.size();
+    ds->nrecs = (const TNode*)(b + o_nrecs);
     ds->node_records = (uint32_t)tnodes.size();
     ds->leaf_records = (uint32_t)tleaves.size();
     ds->nodes_per_leaf = nodes_per_leaf;
@@ -3455,19 +3560,22 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         if (fa.sharedSizeBytes != 0) return fail(GS_ERR_UNSUPPORTED, "render kernel with static LDS");
         const int64_t room = (int64_t)max_lds - (int64_t)lane_lds_bytes(chunked, ds->feat);
         if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
-        uint32_t ln = ds->lds_nodes, ll = ds->lds_leaves, lq = ds->lds_quads;
+        uint32_t ln = ds->lds_nodes, ll = ds->lds_leaves, lq = ds->lds_quads, lr = ds->lds_nrecs;
         auto bytes = [&] {
             return (int64_t)ln * (int64_t)sizeof(TNode) + (int64_t)ll * (int64_t)sizeof(TLeaf) +
-                   (int64_t)lq * (int64_t)sizeof(TQuad);
+                   (int64_t)lq * (int64_t)sizeof(TQuad) + (int64_t)lr * (int64_t)sizeof(TNode);
         };
+        // shrink the least valuable prefix first: quads, then nested records, then all
+        while (bytes() > room && lq) lq = lq - 1 - lq / 16;
+        while (bytes() > room && lr) lr = lr - 1 - lr / 16;
         while (bytes() > room) {
             if (ln) ln = ln - 1 - ln / 16;  // shrink the prefixes until they fit
             if (ll) ll = ll - 1 - ll / 16;
-            if (lq) lq = lq - 1 - lq / 16;
         }
         lc.lds_nodes = ln;
         lc.lds_leaves = ll;
         lc.lds_quads = lq;
+        lc.lds_nrecs = (ds->feat & GS_FEAT_NESTED) ? lr : 0u;
         lc.lds = lane_lds_bytes(chunked, ds->feat) + (size_t)bytes();
         lc.feat = ds->feat;
         if (ln < ds->node_records || ll < ds->leaf_records) lc.feat &= ~GS_FEAT_LDSTREE;
@@ -3481,6 +3589,8 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     a.lds_nodes = lc.lds_nodes;
     a.lds_leaves = lc.lds_leaves;
     a.lds_quads = lc.lds_quads;
+    a.lds_nrecs = lc.lds_nrecs;
+    a.nrecs = ds->nrecs;
     a.lane_nd = lane_nd(chunked, ds->feat);
     const int per_cu = g_blocks_per_cu > 0 ? g_blocks_per_cu : lc.per_cu;
     int64_t blocks = (int64_t)cus * per_cu;
@@ -3593,7 +3703,13 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         return GS_OK;
     }
     if (k_begin) HIPCHK(hipEventRecord(k_begin, st));
-    hipLaunchKernelGGL(kernel_for(va ? GS_FEAT_PILOT : lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
+    // (per-pixel visit counts: the pilot's instantiation, which counts per lane, GS_SALU_COUNT)
+#if defined(GS_STAMPS) || defined(GS_CERT_CHECK)
+    const bool pilot_kernel = va != nullptr;
+#else
+    const bool pilot_kernel = va != nullptr || (GS_SALU_COUNT && outs->item_visits != nullptr);
+#endif
+    hipLaunchKernelGGL(kernel_for(pilot_kernel ? GS_FEAT_PILOT : lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
     if (k_end) HIPCHK(hipEventRecord(k_end, st));
     if (chunk) {
@@ -3683,7 +3799,7 @@ static gs_status pilot_end(gs_device_scene* ds, PilotRun& pr) {
     const ThreadedTree& t = ds->tree;
     std::vector<uint64_t> counts(t.rec.size());
     for (size_t i = 0; i < t.rec.size(); i++) counts[i] = t.leaf[i] ? vis[(size_t)nn + ds->pos[i]] : vis[ds->pos[i]];
-    Placed pl = place_records(t, &counts, ds->n_quads, ds->mirror_budget);
+    Placed pl = place_records(t, &counts, ds->n_quads, ds->mirror_budget, ds->n_nrecs);
     if (pl.tnodes.size() != nn || pl.tleaves.size() != nl) return fail(GS_ERR_HIP, "placement changed the record counts");
     // Nothing of this scene runs on the device yet (the pilot was its first launch and has
     // finished), so the arrays are rewritten in place.
@@ -3697,6 +3813,7 @@ static gs_status pilot_end(gs_device_scene* ds, PilotRun& pr) {
         ds->lds_nodes = pl.lds_nodes;
         ds->lds_leaves = pl.lds_leaves;
         ds->lds_quads = pl.lds_quads;
+        ds->lds_nrecs = pl.lds_nrecs;
         ds->pos = std::move(pl.pos);
         ds->lcfg[0].ready = ds->lcfg[1].ready = false;  // mirror prefixes changed
     }
@@ -3738,7 +3855,8 @@ static gs_status ensure_placement(gs_device_scene* ds, const gs_camera* cam, con
 // The frame context's first frame (and camera changes): every device's pending pilot is
 // launched before any is waited for, so N devices pilot concurrently (internal.hpp).
 gs_status gs_placement_prepare(gs_device_scene* const* scenes, const int* devices, void* const* streams, int n,
-                               const gs_camera* cam, const gs_sample_settings* ss) {
+                               const gs_camera* cam, const gs_sample_settings* ss, int* ran) {
+    *ran = 0;
     std::vector<std::unique_lock<std::mutex>> locks;
     std::vector<PilotRun> runs(n);
     std::vector<int> due(n, 0);
@@ -3753,6 +3871,7 @@ gs_status gs_placement_prepare(gs_device_scene* const* scenes, const int* device
             break;
         }
         due[i] = 1;
+        *ran = 1;
         r = pilot_begin(ds, cam, streams[i], runs[i]);
     }
     for (int i = 0; i < n; i++) {

@@ -16,7 +16,7 @@ gs_status gs_render_tiles_timed_async(const gs_device_scene* ds, const gs_camera
 
 // The placement pilots still pending for a launch of `cam` / `ss` on n devices (scenes[i] on
 // devices[i], its stream streams[i]): every device's pilot is launched before any is waited
-// for, so the first frame of an N-GPU context pilots concurrently (render.hip).  Leaves the
-// current device changed.
+// for, so the first frame of an N-GPU context pilots concurrently (render.hip).  *ran: whether
+// any pilot ran.  Leaves the current device changed.
 gs_status gs_placement_prepare(gs_device_scene* const* scenes, const int* devices, void* const* streams, int n,
-                               const gs_camera* cam, const gs_sample_settings* ss);
+                               const gs_camera* cam, const gs_sample_settings* ss, int* ran);

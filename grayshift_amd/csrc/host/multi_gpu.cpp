@@ -270,9 +270,10 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
         std::vector<void*> st(n);
         for (int i = 0; i < n; i++) sc[i] = dev[i].scene, st[i] = dev[i].stream;
         const auto tp = std::chrono::steady_clock::now();
-        s = gs_placement_prepare(sc.data(), ids.data(), st.data(), n, cam, ss);
+        int ran = 0;
+        s = gs_placement_prepare(sc.data(), ids.data(), st.data(), n, cam, ss, &ran);
         if (s != GS_OK) return s;
-        plan_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
+        if (ran) plan_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
     }
     const bool want_rgb = !out || out->rgb;
     const bool want8 = out && (out->rgb8 || out->ppm_text);

@@ -1,13 +1,17 @@
 #!/bin/bash
-# Round 4, first GPU call: the new GPU tests (batch rounds, robustness), the stamps build's
-# watchdog on the media scenes (the r03 hang), then the adaptive configs A1 / A2 in batch
-# rounds and in the per-lane loop, beside the same scenes at fixed spp.
+# Round 4 GPU call: variant correctness (GS_LIB=variants/r4all.so: SALU visit counts, quad-run
+# lists, nested records in LDS), then A/B against the product library, the stamps build's
+# watchdog on the media scenes (the r03 hang), and the adaptive configs A1 / A2.
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r4a
 mkdir -p $O
-timeout -k 10 500 python -u -m pytest tests/test_gpu_adaptive.py tests/test_gpu_robustness.py tests/test_gpu_placement.py tests/test_gpu_multi.py -x -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { echo "TESTS FAILED"; tail -60 $O/tests.log; exit 1; }
-tail -3 $O/tests.log
+GS_LIB=$R/grayshift_amd/variants/r4all.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_volumes.py tests/test_gpu_instancing_noise.py tests/test_gpu_adaptive.py tests/test_gpu_multi.py tests/test_gpu_placement.py -x -q --timeout 120 --timeout-method thread > $O/tests_r4all.log 2>&1 || { echo "VARIANT TESTS FAILED"; tail -40 $O/tests_r4all.log; exit 1; }
+tail -2 $O/tests_r4all.log
+timeout -k 10 900 python3 -u tools/sweep.py --lib base variants/r4all.so variants/qrun.so variants/salu.so --config final_scene cornell_smoke cornell_box --width 1440 --spp 64 --steps 1 > $O/ab_scenes.txt 2>&1 || { echo "sweep failed"; tail -5 $O/ab_scenes.txt; exit 1; }
+cat $O/ab_scenes.txt
+timeout -k 10 900 python3 -u tools/sweep.py --lib base variants/r4all.so variants/salu.so --config C4 C3 C5 --steps 2 --spp 512 > $O/ab_cfg.txt 2>&1 || { echo "sweep failed"; tail -5 $O/ab_cfg.txt; exit 1; }
+cat $O/ab_cfg.txt
 for sc in cornell_smoke final_scene; do
   GS_LIB=$R/grayshift_amd/variants/stamps.so timeout -k 10 100 python3 -u $R/tools/stamps.py --config $sc --width 96 --spp 4 \
       > $O/stamps_$sc.txt 2> $O/stamps_$sc.err
