@@ -108,8 +108,8 @@ def parse():
     ap.add_argument("--leaf-batch", type=int, default=None)
     ap.add_argument("--node-steps", type=int, default=0, help="node steps per node pass (0: the scene's choice)")
     ap.add_argument("--sample-chunk", type=int, default=None, help="samples per work item (-1 auto, 0 whole pixel)")
-    ap.add_argument("--adaptive-mode", type=int, default=1, choices=[0, 1],
-                    help="adaptive settings: 1 batch rounds (default), 0 the per-lane loop (gs_set_adaptive_mode)")
+    ap.add_argument("--adaptive-mode", type=int, default=1, choices=[0, 1, 2],
+                    help="adaptive settings (gs_set_adaptive_mode): 1 auto (default), 2 batch rounds, 0 the per-lane loop")
     ap.add_argument("--cpu-stride", type=int, default=3,
                     help="CPU baseline / parity subset at N=1: every Nth row and column")
     ap.add_argument("--parity-stride", type=int, default=12, help="parity subset at N>1: every Nth row and column")

@@ -67,10 +67,14 @@ using namespace gsd;
 #define GS_QRUN 0
 #endif
 #define DREF_QRUN 9u
+// Batch rounds (adaptive settings): whole-batch items only for batches up to this size
+#ifndef GS_ROUND_WHOLE_MAX_BATCH
+#define GS_ROUND_WHOLE_MAX_BATCH 256
+#endif
 // The nested trees' records (BVHs under instances) mirrored in LDS after the quads, placed
 // shallowest first (0: read from global memory only)
 #ifndef GS_NESTED_LDS
-#define GS_NESTED_LDS 0
+#define GS_NESTED_LDS 1
 #endif
 #define QRUN_COUNT_SHIFT 22u
 #define QRUN_FIRST_MASK ((1u << QRUN_COUNT_SHIFT) - 1u)
@@ -191,16 +195,21 @@ struct KParams {
     // per leaf record position from visit_leaf_base
     uint32_t* visits;
     uint32_t visit_leaf_base, pad1;
-    // Adaptive settings in batch rounds (per_sample = 1; DESIGN.md §3.2 "Adaptive sampling in
+    // Adaptive settings in batch rounds (rounds = 1; DESIGN.md §3.2 "Adaptive sampling in
     // batch rounds"): launch (round, segment) renders batch `round` of the active packed
-    // pixels active[seg_base, seg_base + seg_n), work item q = (entry q / cpp, samples
-    // [(q % cpp) * chunk, +chunk) of the batch), and every sample's colour goes to
-    // partial[(j * seg_n + entry) * 3] (sample-major: j = the sample's index in the batch);
-    // gs_round_combine_kernel then folds each pixel's batch into its running sums in sample
-    // order (camera.rs:138-147), takes the stop test (:149-164) and lists the pixels that go
-    // on.  gs_round_params_kernel sets the per-round fields from the device-side counts.
+    // pixels active[seg_base, seg_base + seg_n).  gs_round_params_kernel sets the per-round
+    // fields from the device-side counts and picks one of two item forms:
+    //  * whole (many pixels active): item = one pixel's whole batch, run in one lane from the
+    //    pixel's running sums (pstate) exactly as the per-lane loop runs it, then the stop test
+    //    (camera.rs:149-164) in the lane, which writes the colour or the sums and appends the
+    //    pixel to the next round's list;
+    //  * split (per_sample = 1, few pixels left): item q = (entry q / cpp, samples
+    //    [(q % cpp) * chunk, +chunk) of the batch), every sample's colour to partial[(j *
+    //    seg_n + entry) * 3] (sample-major: j = the sample's index in the batch); then
+    //    gs_round_combine_kernel folds each pixel's batch into its sums in sample order
+    //    (camera.rs:138-147) and takes the stop test.
     uint32_t per_sample, round_base, seg_base, seg_n;
-    uint32_t waves, lanes, pad2, pad3;
+    uint32_t waves, lanes, rounds, round;
     const uint32_t* active;    // this round's active packed pixels
     uint32_t* next_active;     // the next round's, appended by the combine
     uint32_t* active_buf[2];   // the two lists (rounds alternate)
@@ -1140,7 +1149,10 @@ __device__ __forceinline__ void count_visit(uint32_t* counts, uint32_t idx) {
 // phases, written to their own debug buffer (the d_item_visits pointer, reinterpreted
 // as u64[3]) — never to an output.  The stamps' fences perturb scheduling, so only the
 // shares are meaningful, not the absolute time.
-#ifdef GS_STAMPS
+#if defined(GS_STAMPS) && defined(GS_STAMP_NOTIME)  // (hang probe: the stamps build without its clock reads)
+#define GS_STAMP(t) do { t = 0; } while (0)
+#define GS_REGION(k, t0) do { } while (0)
+#elif defined(GS_STAMPS)
 #define GS_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); t = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 // Region timing inside divergent shading code: the first active lane adds the wave's
 // elapsed clock to its wave's LDS slot (one count per wave, whatever the mask).
@@ -1425,6 +1437,19 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     st = S_NEED;
                     return;
                 }
+                if (P->rounds) {  // batch rounds: the sums wait for the next round, maybe in another lane
+                    const uint32_t item = LI(L_ITEM);
+                    double* ps = P->pstate + (size_t)item * 5;
+                    ps[0] = LD(L_CSR);
+                    ps[1] = LD(L_CSG);
+                    ps[2] = LD(L_CSB);
+                    ps[3] = lsum;
+                    ps[4] = lsq;
+                    P->next_active[atomicAdd(&P->round_counts[P->round + 1u], 1u)] = item;
+                    if ((c_nodes | c_sph) >= (1u << 30)) flush_counts();
+                    st = S_NEED;
+                    return;
+                }
                 LD(L_SCOUNT) = scount + (double)P->ss.batch_size;
                 LI(L_BLEFT) = P->ss.batch_size;
             }
@@ -1468,6 +1493,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0, acc_refill = 0, acc_trav = 0, acc_shade = 0;
     uint64_t acc_node = 0, acc_leaf = 0;  // stamps build: wave clock in node / leaf passes
     uint64_t dist_ref = 0, dist_kind = 0;  // stamps build: distinct leaf refs / ref kinds per leaf pass
+    uint64_t dist_bad = 0;                 // stamps build: those counts' loops that did not converge
     uint64_t it_all = 0, it_node = 0, it_leaf = 0, ln_node = 0, ln_leaf = 0, it_shade = 0, ln_shade = 0;
     // stamps build: node steps (lanes) from global memory; wave node steps with any active lane,
     // with any lane reading its record from global memory; active lanes over those steps
@@ -1558,7 +1584,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     const uint32_t qr = fine ? q32 - P->fine_base : q32;
                     const uint32_t pr = udiv(qr, fine ? P->u_fcpp : P->u_cpp), ck = qr - pr * cpp;
                     uint32_t slot, x, y;
-                    if (P->per_sample) {  // batch rounds: the packed pixel of active entry pr
+                    if (P->rounds) {  // batch rounds: the packed pixel of active entry pr
                         const uint32_t it = P->active[P->seg_base + pr];
                         slot = udiv(it, P->u_tpx);
                         const uint32_t w = it - slot * tile_px;
@@ -1617,6 +1643,25 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                             LI(L_SAMPLE) = ck * csz;
                             LI(L_BLEFT) = min(csz, P->ss.batch_size - ck * csz);
                             if (ck == 0) atomicAdd(&s_cnt[C_PIX], 1ull);
+                        } else if (P->rounds) {
+                            // batch rounds, whole-batch items: the pixel's running sums (none
+                            // before round 1), then batch `round` in this lane
+                            if (P->round_base) {
+                                const double* ps = P->pstate + (size_t)item * 5;
+                                LD(L_CSR) = ps[0];
+                                LD(L_CSG) = ps[1];
+                                LD(L_CSB) = ps[2];
+                                LD(L_LSUM) = ps[3];
+                                LD(L_LSQ) = ps[4];
+                            } else {
+                                LD(L_LSUM) = 0.0;
+                                LD(L_LSQ) = 0.0;
+                            }
+                            // sample_count after this batch: 0.0 + bs + ... (exact integers)
+                            LD(L_SCOUNT) = (double)((uint64_t)P->round_base + P->ss.batch_size);
+                            LI(L_ITEM) = item;
+                            LI(L_BLEFT) = P->ss.batch_size;
+                            LI(L_SAMPLE) = P->round_base;
                         } else {
                             LD(L_LSUM) = 0.0;
                             LD(L_LSQ) = 0.0;
@@ -1713,7 +1758,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 auto node_step = [&](auto fast_tag, auto ldsp_tag) __attribute__((always_inline)) {
                 constexpr bool FAST = decltype(fast_tag)::value;
                 constexpr bool LDSP = decltype(ldsp_tag)::value;
-#ifdef GS_STAMPS
+#if defined(GS_STAMPS) && !defined(GS_STAMP_NOPASS)
                 {
                     const bool glob = !((FEAT & GS_FEAT_LDSTREE) != 0) && cur < THR_END && cur >= (A.lds_nodes << 5);
                     const uint64_t act = __builtin_amdgcn_ballot_w64(LDSP ? cur < lim : cur < THR_END);
@@ -1845,22 +1890,41 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 if constexpr ((FEAT & GS_FEAT_VISITS) != 0) {
                     if (P->visits) count_visit(P->visits, P->visit_leaf_base + (cur & ~THR_LEAF));
                 }
-#ifdef GS_STAMPS
+#if defined(GS_STAMPS) && !defined(GS_STAMP_NOPASS)
                 {  // counted by the pass's first active lane (summed over lanes at the end)
-                    const uint64_t act = __builtin_amdgcn_ballot_w64(true);
+                    // The r03 hang of this build on media scenes was this loop: in the media
+                    // kernels (SGPRs spilled to VGPR lanes, scratch reloads in flight) the
+                    // compiler's wait before the loop left the leaf record's last load in
+                    // flight on the global-memory path, so v_readlane and the compare inside
+                    // the loop could read `ref` at different times and the lane the loop is
+                    // trying to retire never matched (a waitcnt hazard in the diagnostic code
+                    // only: the product kernels have no such loop over a freshly loaded value).
+                    // Now every load is waited for first, and the loop is bounded (a pass that
+                    // would not converge is counted in dbg[23]).
+#ifndef GS_STAMP_DIST_NOWAIT  // (probe builds: without the wait / without the bound)
+                    __builtin_amdgcn_s_waitcnt(0);
+#endif
+#ifdef GS_STAMP_DIST_UNBOUNDED
+#define GS_DIST_BOUND 0x7FFFFFFF
+#else
+#define GS_DIST_BOUND 64
+#endif
+                    const uint64_t act = __builtin_amdgcn_read_exec();
                     const bool first = __builtin_ctzll(act) == (uint32_t)lane;
                     uint64_t m = act;
-                    while (m) {
+                    for (int it = 0; it < GS_DIST_BOUND && m; it++) {
                         const uint32_t r0 = __builtin_amdgcn_readlane(ref, __builtin_ctzll(m));
                         m &= ~__builtin_amdgcn_ballot_w64(ref == r0);
                         dist_ref += first;
                     }
+                    dist_bad += (m != 0) && first;
                     m = act;
-                    while (m) {
+                    for (int it = 0; it < GS_DIST_BOUND && m; it++) {
                         const uint32_t k0 = __builtin_amdgcn_readlane(ref, __builtin_ctzll(m)) >> GS_REF_SHIFT;
                         m &= ~__builtin_amdgcn_ballot_w64((ref >> GS_REF_SHIFT) == k0);
                         dist_kind += first;
                     }
+                    dist_bad += (m != 0) && first;
                 }
 #endif
                 auto sphere_leaf = [&]() __attribute__((always_inline)) {  // a stationary sphere, inline
@@ -2105,10 +2169,11 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #endif
     }
 #ifdef GS_STAMPS
-    if (P->item_visits && (dist_ref || dist_kind)) {
+    if (P->item_visits && (dist_ref || dist_kind || dist_bad)) {
         unsigned long long* dbg = (unsigned long long*)P->item_visits;
         atomicAdd(&dbg[17], (unsigned long long)dist_ref);
         atomicAdd(&dbg[18], (unsigned long long)dist_kind);
+        atomicAdd(&dbg[23], (unsigned long long)dist_bad);
     }
     if (P->item_visits && d_gvis) atomicAdd(&((unsigned long long*)P->item_visits)[19], (unsigned long long)d_gvis);
     if (lane == 0 && P->item_visits) {
@@ -2268,12 +2333,17 @@ __global__ void gs_round_init_kernel(const KParams* __restrict__ P) {
 // chunking (finer when few pixels are left, so the round's samples still spread over the
 // lanes), queue claim and cleared queue.
 __global__ void gs_round_params_kernel(KParams* __restrict__ P, uint32_t round, uint32_t seg, uint32_t seg_px,
-                                       int32_t chunk_req) {
+                                       int32_t chunk_req, int32_t whole_mode) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const uint32_t n_act = P->round_counts[round];
     const uint32_t base = seg * seg_px;
     const uint32_t n_seg = n_act > base ? min(seg_px, n_act - base) : 0u;
     const uint32_t bs = P->ss.batch_size;
+    // whole-batch items while the active pixels are at least twice the lanes (no per-sample
+    // colours kept, no combine), split ones once few are left (their samples spread over the
+    // lanes); a requested sample chunk always splits
+    const bool whole = chunk_req <= 0 && bs <= GS_ROUND_WHOLE_MAX_BATCH &&
+                       (whole_mode > 0 || (whole_mode < 0 && (uint64_t)n_seg >= 2ull * P->lanes));
     uint32_t csz;
     if (chunk_req > 0) {
         csz = min((uint32_t)chunk_req, bs);
@@ -2281,8 +2351,10 @@ __global__ void gs_round_params_kernel(KParams* __restrict__ P, uint32_t round, 
         csz = min(16u, bs);
         while (csz > 1u && (uint64_t)n_seg * ((bs + csz - 1u) / csz) < 8ull * P->lanes) csz >>= 1;
     }
-    const uint32_t cpp = (bs + csz - 1u) / csz;
-    P->chunk = csz;
+    const uint32_t cpp = whole ? 1u : (bs + csz - 1u) / csz;
+    P->per_sample = whole ? 0u : 1u;
+    P->chunk = whole ? 0u : csz;
+    P->round = round;
     P->cpp = cpp;
     P->u_cpp = udiv_make(cpp);
     P->n_items = n_seg * cpp;
@@ -2302,6 +2374,7 @@ __global__ void gs_round_params_kernel(KParams* __restrict__ P, uint32_t round, 
 // sums in sample order (camera.rs:142-146), then the stop test (:149-164) exactly as the
 // per-lane loop takes it; a stopped pixel's colour (:167) is written, the rest go on.
 __global__ void gs_round_combine_kernel(const KParams* __restrict__ P, uint32_t round) {
+    if (!P->per_sample) return;  // a whole-batch round: the lanes took the stop test
     const uint32_t n = P->seg_n, bs = P->ss.batch_size, lane = threadIdx.x & 63u;
     const uint32_t span = (n + 63u) & ~63u;
     const double confidence_sq = P->ss.confidence * P->ss.confidence;
@@ -2411,7 +2484,20 @@ static int32_t g_placement = 1;  // 1: placement pilot at a scene's first launch
 static uint64_t g_partial_budget = 4ull << 30;  // auto chunks: at most 4 GiB of chunk sums (per launch slot)
 // Adaptive settings (more than one batch): 1 = batch rounds (gs_round_*_kernel), 0 = the
 // per-lane loop (one work item per pixel running every batch).  Bit-identical results.
-static int32_t g_adaptive_rounds = 1;
+static int32_t g_adaptive_rounds = 1;  // 1 auto (GS_ROUND_MIN_CAP), 2 always rounds, 0 never
+// Work items of a round: 0 split (default; measured on MI355X, A2 cornell_box 1024^2: split
+// 7520, whole-batch items while the active pixels fill the lanes twice 5910 Msamples/s;
+// A1 hdri 19738 vs 18124), 1 whole-batch items, -1 whole while the active pixels fill the
+// lanes twice.
+static int32_t g_round_whole = 0;
+// Auto mode: batch rounds when a pixel can take at least this many samples ((max_samples /
+// batch + 1) x batch): the per-lane loop's tail is up to that many samples in one lane.
+// MI355X: A2 cornell_box (cap 1024) rounds 7520 vs per-lane 5394 Msamples/s; A1 hdri (cap
+// 256) rounds 19738 vs per-lane 24582 -- its pixels stop after one or two batches, and the
+// rounds' per-sample colours and launches cost more than its short tail.
+#ifndef GS_ROUND_MIN_CAP
+#define GS_ROUND_MIN_CAP 512
+#endif
 static const uint64_t kMaxRounds = 1u << 16;  // more batches than this: the per-lane loop
 
 extern "C" void gs_set_last_error(const char* msg) { tl_err = msg ? msg : ""; }
@@ -2849,8 +2935,15 @@ gs_status gs_set_placement(int32_t mode) {
 }
 
 gs_status gs_set_adaptive_mode(int32_t mode) {
-    if (mode != 0 && mode != 1) return fail(GS_ERR_ARG, "adaptive mode is 0 (per-lane loop) or 1 (batch rounds)");
+    if (mode < 0 || mode > 2)
+        return fail(GS_ERR_ARG, "adaptive mode is 0 (per-lane loop), 1 (auto) or 2 (batch rounds)");
     g_adaptive_rounds = mode;
+    return GS_OK;
+}
+
+gs_status gs_debug_set_round_items(int32_t mode) {
+    if (mode < -1 || mode > 1) return fail(GS_ERR_ARG, "round item mode is -1 (auto), 0 (split) or 1 (whole)");
+    g_round_whole = mode;
     return GS_OK;
 }
 
@@ -3500,19 +3593,26 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     // pixel can run (the loop ends once sample_count > max_samples, camera.rs:162), in
     // segments of at most seg_px active pixels whose per-sample colours fit the budget.
     uint32_t n_rounds = 0, seg_px = 0, n_segs = 0;
-    if (g_adaptive_rounds && g_sample_chunk != 0 && ss->max_samples >= ss->batch_size && !outs->item_visits && !va) {
+#if defined(GS_STAMPS) || defined(GS_CERT_CHECK)
+    const bool visit_out = false;  // (those builds' item_visits is their record buffer: rounds allowed)
+#else
+    const bool visit_out = outs->item_visits != nullptr;
+#endif
+    if (g_adaptive_rounds && g_sample_chunk != 0 && ss->max_samples >= ss->batch_size && !visit_out && !va) {
         const uint64_t R = (uint64_t)ss->max_samples / ss->batch_size + 1u;
         const uint64_t sp = std::min<uint64_t>((uint64_t)cap, g_partial_budget / ((uint64_t)ss->batch_size * 24u));
-        if (R <= kMaxRounds && sp >= 1 && sp * ss->batch_size < 0x7FFFFFFFull) {
+        const bool want = g_adaptive_rounds == 2 || R * ss->batch_size >= GS_ROUND_MIN_CAP;
+        if (want && R <= kMaxRounds && sp >= 1 && sp * ss->batch_size < 0x7FFFFFFFull) {
             n_rounds = (uint32_t)R;
             seg_px = (uint32_t)sp;
             n_segs = (uint32_t)(((uint64_t)cap + sp - 1) / sp);
-            chunk = 1;  // (the chunked lane layout; each round's chunking is set on the device)
+            chunk = 0;  // (the adaptive lane layout: whole-batch rounds keep Σlum, Σlum², the count)
             cpp = 1;
             fine_px = (uint32_t)cap, fine_chunk = 1, fine_cpp = 1;
         }
     }
     kp.per_sample = n_rounds ? 1u : 0u;
+    kp.rounds = n_rounds ? 1u : 0u;
     kp.chunk = chunk;
     kp.cpp = cpp;
     kp.fine_px = fine_px;
@@ -3639,7 +3739,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     }
     LaunchSlot& sl = mds->slots[pick];
     if (sl.used && sl.stream != st) HIPCHK(hipStreamWaitEvent(st, sl.done, 0));
-    if (chunk) {
+    if (chunk || n_rounds) {
         const size_t need = need_partial;
         if (sl.partial_bytes < need) {
             if (sl.used) HIPCHK(hipEventSynchronize(sl.done));  // nothing in flight reads it
@@ -3691,7 +3791,8 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         const unsigned g_comb = (unsigned)std::min<int64_t>((seg_px + 255) / 256, 8192);
         for (uint32_t r = 0; r < n_rounds; r++)
             for (uint32_t sg = 0; sg < n_segs; sg++) {
-                hipLaunchKernelGGL(gs_round_params_kernel, dim3(1), dim3(64), 0, st, dP, r, sg, seg_px, g_sample_chunk);
+                hipLaunchKernelGGL(gs_round_params_kernel, dim3(1), dim3(64), 0, st, dP, r, sg, seg_px, g_sample_chunk,
+                                   g_round_whole);
                 hipLaunchKernelGGL(kernel_for(lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
                 hipLaunchKernelGGL(gs_round_combine_kernel, dim3(g_comb), dim3(256), 0, st, (const KParams*)dP, r);
             }

@@ -255,15 +255,24 @@ gs_status gs_debug_record_visits(const gs_device_scene* scene, const gs_camera* 
                                  float* d_packed_rgb, uint32_t* d_visits, void* stream);
 
 /* Adaptive settings (ABI 8) -- SampleSettings that run more than one batch
- * (max_samples >= batch_size, camera.rs:135-165).  1 (default): batch rounds -- round r
- * renders batch r of every pixel still active, its samples spread over the lanes like the
- * fixed-spp chunks, each sample's colour kept; a combine pass then adds each pixel's batch
- * into its running sums in sample order and takes the reference's stop test, so the
- * result is bit-identical to the per-lane loop.  A launch then issues a few small kernels
- * per round on its stream (no host synchronisation).  0: the per-lane loop (one work item
- * per pixel running all of its batches; also used for more than 65536 possible batches,
- * a sample chunk of 0, or the diagnostic per-pixel visit output). */
+ * (max_samples >= batch_size, camera.rs:135-165).  Batch rounds: round r renders batch r of
+ * every pixel still active, its samples spread over the lanes like the fixed-spp chunks,
+ * each sample's colour kept; a combine pass then adds each pixel's batch into its running
+ * sums in sample order and takes the reference's stop test, so the result is
+ * bit-identical to the per-lane loop.  A launch then issues a few small kernels per round
+ * on its stream (no host synchronisation).  The per-lane loop: one work item per pixel
+ * running all of its batches.  mode 1 (default): rounds when a pixel can take 512 samples
+ * or more ((max_samples / batch + 1) x batch: the per-lane loop's tail), else the loop;
+ * 2: always rounds; 0: always the loop.  The loop also serves more than 65536 possible
+ * batches, a sample chunk of 0 and the diagnostic per-pixel visit output. */
 gs_status gs_set_adaptive_mode(int32_t mode);
+
+/* Test hook (ABI 8): the work items of batch rounds.  0 (default): each batch split into
+ * sample chunks whose colours a combine pass folds in order.  1: each pixel's batch as one
+ * item (from its running sums, the stop test in the lane: no per-sample colours; batches up
+ * to 256).  -1: whole-batch items while a round's active pixels are at least twice the
+ * device's lanes, split after.  Every choice renders the same bits. */
+gs_status gs_debug_set_round_items(int32_t mode);
 
 /* Test hook: the auto sample-chunk rule's budget for chunk sums (default 4 GiB; 0
  * restores it).  A smaller budget makes renders take the chunk-doubling branch. */

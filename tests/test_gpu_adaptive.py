@@ -25,25 +25,32 @@ TOL = 1e-3
 
 
 class _mode:
-    def __init__(self, mode, chunk=-1, budget=0):
-        self.mode, self.chunk, self.budget = mode, chunk, budget
+    def __init__(self, mode, chunk=-1, budget=0, items=0):
+        self.mode, self.chunk, self.budget, self.items = mode, chunk, budget, items
 
     def __enter__(self):
         N.check(N.lib.gs_set_adaptive_mode(self.mode))
         g.set_tuning(52, 0, 0, self.chunk)
         N.check(N.lib.gs_debug_set_partial_budget(self.budget))
+        N.check(N.lib.gs_debug_set_round_items(self.items))
 
     def __exit__(self, *a):
         N.check(N.lib.gs_set_adaptive_mode(1))
         g.set_tuning(52, 0, 0, -1)
         N.check(N.lib.gs_debug_set_partial_budget(0))
+        N.check(N.lib.gs_debug_set_round_items(0))
 
 
 def _both(sc, seed, **kw):
-    with _mode(1, **kw):
+    """Batch rounds (split items at these small sizes) and the per-lane loop; also asserts the
+    whole-batch round items render the same frame."""
+    with _mode(2, **kw):
         a, ca = g.render(sc, seed=seed)
     with _mode(0):
         b, cb = g.render(sc, seed=seed)
+    with _mode(2, items=1):
+        w, cw = g.render(sc, seed=seed)
+    assert np.array_equal(w, b) and cw == cb
     return a, ca, b, cb
 
 
@@ -88,10 +95,10 @@ def test_round_chunks_and_segments(chunk):
     (the active list rendered in segments): the same frame."""
     sc = scenes.cornell_box(width=48)
     ref, rc = _both(sc, seed=7)[2:]
-    with _mode(1, chunk=chunk):
+    with _mode(2, chunk=chunk):
         a, ca = g.render(sc, seed=7)
     assert np.array_equal(a, ref) and ca == rc
-    with _mode(1, chunk=chunk, budget=100 * sc.settings.batch_size * 24):
+    with _mode(2, chunk=chunk, budget=100 * sc.settings.batch_size * 24):
         s, cs = g.render(sc, seed=7)
     assert np.array_equal(s, ref) and cs == rc
 
@@ -133,5 +140,22 @@ def test_round_partition_invariance(world, tile):
 
 
 def test_adaptive_mode_rejects_bad_values():
-    assert N.lib.gs_set_adaptive_mode(2) == N.GS_ERR_ARG
+    assert N.lib.gs_set_adaptive_mode(3) == N.GS_ERR_ARG
     assert N.lib.gs_set_adaptive_mode(-1) == N.GS_ERR_ARG
+    assert N.lib.gs_debug_set_round_items(2) == N.GS_ERR_ARG
+
+
+@pytest.mark.parametrize("items", [0, 1, -1])
+def test_round_items_at_a_chip_filling_size(items):
+    """cornell_box at 768 x 768 (590 k pixels: above twice the device's 262 k lanes, so item
+    rule -1 runs whole-batch items in the first round and split ones later), split (0) and
+    whole (1) items, and the default auto mode: the per-lane loop's frame every time."""
+    sc = scenes.cornell_box(width=768)
+    with _mode(0):
+        ref, rc = g.render(sc, seed=9)
+    with _mode(2, items=items):
+        a, ca = g.render(sc, seed=9)
+    with _mode(1):
+        auto, cauto = g.render(sc, seed=9)
+    assert np.array_equal(a, ref) and ca == rc
+    assert np.array_equal(auto, ref) and cauto == rc

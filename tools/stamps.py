@@ -46,6 +46,9 @@ def main():
     print("node steps: %d wave steps (%.1f active lanes), %.1f%% with a lane reading global memory; "
           "%.1f%% of lane node visits from global memory" % (
               wsteps, wlanes / max(1, wsteps), 100.0 * wsteps_g / max(1, wsteps), 100.0 * gvis / max(1, wlanes)))
+    bad = int(dbg[23].item())
+    if bad:
+        print("WARNING: %d leaf passes whose distinct-ref count did not converge in 64 steps" % bad)
     reg = dbg[10:15].cpu().tolist()
     # split shading (no GS_FEAT_MIXED) stamps background / reconstruct / scatter on their own;
     # staged shading (GS_FEAT_MIXED, media, nested) stamps all of it as region 2
