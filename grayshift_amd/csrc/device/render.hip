@@ -1892,39 +1892,33 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 }
 #if defined(GS_STAMPS) && !defined(GS_STAMP_NOPASS)
                 {  // counted by the pass's first active lane (summed over lanes at the end)
-                    // The r03 hang of this build on media scenes was this loop: in the media
-                    // kernels (SGPRs spilled to VGPR lanes, scratch reloads in flight) the
-                    // compiler's wait before the loop left the leaf record's last load in
-                    // flight on the global-memory path, so v_readlane and the compare inside
-                    // the loop could read `ref` at different times and the lane the loop is
-                    // trying to retire never matched (a waitcnt hazard in the diagnostic code
-                    // only: the product kernels have no such loop over a freshly loaded value).
-                    // Now every load is waited for first, and the loop is bounded (a pass that
-                    // would not converge is counted in dbg[23]).
-#ifndef GS_STAMP_DIST_NOWAIT  // (probe builds: without the wait / without the bound)
-                    __builtin_amdgcn_s_waitcnt(0);
-#endif
-#ifdef GS_STAMP_DIST_UNBOUNDED
-#define GS_DIST_BOUND 0x7FFFFFFF
-#else
-#define GS_DIST_BOUND 64
-#endif
+                    // The r03 hang of this build on media scenes was in these counts.  Round-4
+                    // probes (profiles/r04/stamps_hang_probes.txt): waiting for every load first
+                    // did not help (still hung), bounding the loops did, and the bounded runs
+                    // showed the distinct-REF loop converging (cornell_smoke: 1.00 distinct refs
+                    // per pass) while a second loop over the refs' KINDS, the same ballot/readlane
+                    // pattern on `ref >> GS_REF_SHIFT`, did not (16.8 "kinds" where every lane
+                    // held one ref): its compare never matched the lane it read in the media
+                    // kernels (SGPRs spilled to VGPR lanes there), so its mask never emptied.  The
+                    // kinds are now collected from the converging loop's uniform refs, the picked
+                    // lane is always retired (<= 64 steps whatever a ballot returns), and a pass
+                    // whose ballot missed its own lane is counted in dbg[23].
                     const uint64_t act = __builtin_amdgcn_read_exec();
                     const bool first = __builtin_ctzll(act) == (uint32_t)lane;
+                    bool bad = false;
+                    uint32_t kinds = 0;
                     uint64_t m = act;
-                    for (int it = 0; it < GS_DIST_BOUND && m; it++) {
-                        const uint32_t r0 = __builtin_amdgcn_readlane(ref, __builtin_ctzll(m));
-                        m &= ~__builtin_amdgcn_ballot_w64(ref == r0);
+                    while (m) {
+                        const uint32_t L = (uint32_t)__builtin_ctzll(m);
+                        const uint32_t r0 = __builtin_amdgcn_readlane(ref, L);
+                        const uint64_t same = __builtin_amdgcn_ballot_w64(ref == r0);
+                        bad |= ((same >> L) & 1u) == 0;
+                        kinds |= 1u << (r0 >> GS_REF_SHIFT);
+                        m &= ~(same | (1ull << L));
                         dist_ref += first;
                     }
-                    dist_bad += (m != 0) && first;
-                    m = act;
-                    for (int it = 0; it < GS_DIST_BOUND && m; it++) {
-                        const uint32_t k0 = __builtin_amdgcn_readlane(ref, __builtin_ctzll(m)) >> GS_REF_SHIFT;
-                        m &= ~__builtin_amdgcn_ballot_w64((ref >> GS_REF_SHIFT) == k0);
-                        dist_kind += first;
-                    }
-                    dist_bad += (m != 0) && first;
+                    dist_kind += first ? (uint64_t)__builtin_popcount(kinds) : 0;
+                    dist_bad += bad && first;
                 }
 #endif
                 auto sphere_leaf = [&]() __attribute__((always_inline)) {  // a stationary sphere, inline

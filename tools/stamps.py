@@ -48,7 +48,7 @@ def main():
               wsteps, wlanes / max(1, wsteps), 100.0 * wsteps_g / max(1, wsteps), 100.0 * gvis / max(1, wlanes)))
     bad = int(dbg[23].item())
     if bad:
-        print("WARNING: %d leaf passes whose distinct-ref count did not converge in 64 steps" % bad)
+        print("WARNING: %d leaf passes whose exec mask held lanes outside the ballot (their distinct-ref / kind counts are not trusted)" % bad)
     reg = dbg[10:15].cpu().tolist()
     # split shading (no GS_FEAT_MIXED) stamps background / reconstruct / scatter on their own;
     # staged shading (GS_FEAT_MIXED, media, nested) stamps all of it as region 2
