@@ -151,6 +151,7 @@ extern "C" {
     pub fn gs_set_placement(mode: i32) -> gs_status;
     pub fn gs_set_adaptive_mode(mode: i32) -> gs_status;
     pub fn gs_debug_set_round_items(mode: i32) -> gs_status;
+    pub fn gs_debug_set_cube_lists(on: i32) -> gs_status;
     pub fn gs_debug_record_visits(scene: *const gs_device_scene, cam: *const gs_camera, ss: *const gs_sample_settings,
                                   seed: u64, part: *const gs_partition, d_packed_rgb: *mut f32, d_visits: *mut u32,
                                   stream: *mut c_void) -> gs_status;

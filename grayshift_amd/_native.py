@@ -164,6 +164,7 @@ SIGNATURES = {
     "gs_set_placement": (C.c_int32, [C.c_int32]),
     "gs_set_adaptive_mode": (C.c_int32, [C.c_int32]),
     "gs_debug_set_round_items": (C.c_int32, [C.c_int32]),
+    "gs_debug_set_cube_lists": (C.c_int32, [C.c_int32]),
     "gs_debug_record_visits": (C.c_int32, [_P, C.POINTER(gs_camera), C.POINTER(gs_sample_settings), C.c_uint64,
                                            C.POINTER(gs_partition), _P, _P, _P]),
     "gs_device_scene_create": (C.c_int32, [_P, C.POINTER(_P)]),

@@ -125,13 +125,22 @@ def main(argv=None):
                     help="print per-kernel VGPR/SGPR/LDS/occupancy (hipcc remarks)")
     a = ap.parse_args(argv)
     extra = ["-Rpass-analysis=kernel-resource-usage"] if a.resource_usage else []
-    build_product(force=a.force or a.resource_usage, verbose=a.verbose, extra=extra)
-    for spec in a.variant:
+    import concurrent.futures as cf
+
+    def variant(spec):
         name, _, flags = spec.partition(":")
         path = os.path.join(HERE, "variants", name + ".so")
         os.makedirs(os.path.dirname(path), exist_ok=True)
         build_product(force=True, verbose=a.verbose, extra=extra + flags.split(), out=path)
-        print("variant", path, flags)
+        return "variant %s %s" % (path, flags)
+
+    # the product and the variants side by side (each compile is one process; 4 at a time)
+    with cf.ThreadPoolExecutor(max_workers=4) as ex:
+        jobs = [ex.submit(build_product, force=a.force or a.resource_usage, verbose=a.verbose, extra=extra)]
+        jobs += [ex.submit(variant, spec) for spec in a.variant]
+        for j in jobs[1:]:
+            print(j.result())
+        jobs[0].result()
     if not a.no_oracle:
         build_oracle(force=a.force, verbose=a.verbose)
         build_kat(force=a.force, verbose=a.verbose)

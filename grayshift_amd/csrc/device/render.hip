@@ -143,8 +143,9 @@ struct DevScene {
     const gs_msphere* mspheres;
     const gs_quad* quads;
     const gs_triangle* tris;
-    const gs_list* lists;
+    const gs_list* lists;       // (a Quad::cube list: {cube index, GS_CUBE_FLAG | first quad}, cube_test)
     const uint32_t* list_refs;
+    const double* cubes;        // GS_CUBE_DOUBLES per Quad::cube list (cube_test)
     const gs_instance* inst;
     const gs_medium* media;
     const uint8_t* noise_perm;  // 256 B, Perlin::default()'s table (NoiseTexture)
@@ -451,10 +452,143 @@ __device__ __forceinline__ u32x4 quad_part(const QuadSrc& qs, uint32_t i, uint32
         return *(lds_u32x4*)(qs.lds + i * (uint32_t)sizeof(TQuad) + ((GS_QUAD_SWZ ? (k ^ (i & 7u)) : k) << 4));
     return sp<UNI>(reinterpret_cast<const u32x4*>(qs.g + i))[k];
 }
+// Axis-aligned quads (GS_AQUAD; every Quad::cube face, quad.rs:54-80, the Cornell walls,
+// the lights): the plane's normal is +-e_a and u, v each have one non-zero component, on
+// the two other axes iu, iv.  Every term of the reference's dot and cross products that
+// multiplies a zero component is then a zero, and adding a zero to a non-zero value is
+// exact, so Quad::hit's values reduce to (TQuad's aligned form, set up by aligned_tquad):
+//   t     = (D' - o_a) / d_a                        (D' = n_a D; plane.rs:21-29, |den| = |d_a|)
+//   alpha = W' (p_iu V_iv),  beta = W' (U_iu p_iv)  (W' = +-w_a: the cross products' sign)
+//   p_k   = (o_k + d_k t) - Q_k                     (ray.at(t) - q, quad.rs:86-88)
+// with the same roundings as the full test: the same t, alpha and beta, bit for bit,
+// except that where the full test's value is a zero its sign may differ -- no comparison
+// (0 <= alpha, tmin <= t) and no later use tells a zero's sign apart.  The record's first
+// word is a signalling-NaN tag (no arithmetic result, and the host re-tags a full record
+// that would collide) carrying the axes: code = 2 a + o, o = 0: (iu, iv) = (a+1, a+2) mod
+// 3, o = 1: the other order.  Layout: [tag|code, D'], [Q_iu, Q_iv], [U_iu, V_iv], [W', 0].
+#ifndef GS_AQUAD
+#define GS_AQUAD 0  // single quads in the aligned form (dynamic selects: measured slower, profiles/r04/ab_aligned_quads.txt)
+#endif
+#ifndef GS_AQ_UNIFORM
+#define GS_AQ_UNIFORM 0  // 1: a wave-uniform axis code runs a compile-time copy (no selects)
+#endif
+#define GS_AQ_TAG 0xFFF4A5C0u
+template <bool UNI, class Pick>
+__device__ __forceinline__ bool aquad_accept(const QuadSrc& qs, uint32_t i, double Dp, Pick pick, double tmin,
+                                             double tmax, double& t_out) {
+    double oa, da, ou, du, ov, dv;
+    pick(oa, da, ou, du, ov, dv);
+    if (fabs(da) < 1e-8) return false;
+    const double t = (Dp - oa) / da;
+    if (!(tmin <= t && t <= tmax)) return false;
+    const u32x4 b = quad_part<UNI>(qs, i, 1), c = quad_part<UNI>(qs, i, 2), e = quad_part<UNI>(qs, i, 3);
+    const double pu = (ou + du * t) - lo_hi(b.x, b.y);
+    const double pv = (ov + dv * t) - lo_hi(b.z, b.w);
+    const double W = lo_hi(e.x, e.y);
+    const double alpha = W * (pu * lo_hi(c.z, c.w));
+    const double beta = W * (lo_hi(c.x, c.y) * pv);
+    if (!(0.0 <= alpha && alpha <= 1.0) || !(0.0 <= beta && beta <= 1.0)) return false;
+    t_out = t;
+    return true;
+}
+__device__ __forceinline__ double d3_at(const d3& v, uint32_t k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+template <int CODE>
+__device__ __forceinline__ double d3_c(const d3& v, int which) {  // which: 0 = a, 1 = iu, 2 = iv
+    constexpr int A = CODE >> 1, O = CODE & 1;
+    const int k = which == 0 ? A : (which == 1 ? (A + 1 + O) % 3 : (A + 2 - O) % 3);
+    return k == 0 ? v.x : (k == 1 ? v.y : v.z);
+}
+template <bool UNI, int CODE>
+__device__ __forceinline__ bool aquad_fixed(const QuadSrc& qs, uint32_t i, double Dp, const Ray& ray, double tmin,
+                                            double tmax, double& t_out) {
+    return aquad_accept<UNI>(
+        qs, i, Dp,
+        [&](double& oa, double& da, double& ou, double& du, double& ov, double& dv) {
+            oa = d3_c<CODE>(ray.o, 0);
+            da = d3_c<CODE>(ray.d, 0);
+            ou = d3_c<CODE>(ray.o, 1);
+            du = d3_c<CODE>(ray.d, 1);
+            ov = d3_c<CODE>(ray.o, 2);
+            dv = d3_c<CODE>(ray.d, 2);
+        },
+        tmin, tmax, t_out);
+}
 template <bool UNI>
 __device__ __forceinline__ bool quad_test(const QuadSrc& qs, uint32_t i, const Ray& ray, double tmin, double tmax,
                                           double& t_out) {
-    const u32x4 a = quad_part<UNI>(qs, i, 0), b = quad_part<UNI>(qs, i, 1);
+    const u32x4 a = quad_part<UNI>(qs, i, 0);
+#if GS_AQUAD
+    if ((a.y & ~7u) == GS_AQ_TAG) {
+        const uint32_t code = a.y & 7u;
+        const double Dp = lo_hi(a.z, a.w);
+#if GS_AQ_UNIFORM == 2
+        // Waterfall over the wave's axis codes (one in a box list's lockstep walk, where
+        // every lane is at the same face of its box): the lanes of the first remaining code
+        // copy their ray's components under a scalar branch (register moves, no selects),
+        // then run the one copy of the test.
+        bool res = false;
+#pragma unroll 1
+        for (;;) {
+            const uint32_t c0 = UNI ? code : __builtin_amdgcn_readfirstlane(code);
+            if (code == c0) {
+                double oa, da, ou, du, ov, dv;
+#define GS_AQ_CASE(C)                                                                       \
+    case C:                                                                                 \
+        __asm__ volatile("" ::: "memory");                                                  \
+        oa = d3_c<C>(ray.o, 0), da = d3_c<C>(ray.d, 0), ou = d3_c<C>(ray.o, 1);           \
+        du = d3_c<C>(ray.d, 1), ov = d3_c<C>(ray.o, 2), dv = d3_c<C>(ray.d, 2);           \
+        break;
+                switch (c0) {
+                    GS_AQ_CASE(0)
+                    GS_AQ_CASE(1)
+                    GS_AQ_CASE(2)
+                    GS_AQ_CASE(3)
+                    GS_AQ_CASE(4)
+                    default:
+                    GS_AQ_CASE(5)
+                }
+#undef GS_AQ_CASE
+                res = aquad_accept<UNI>(
+                    qs, i, Dp,
+                    [&](double& a0, double& a1, double& a2, double& a3, double& a4, double& a5) {
+                        a0 = oa, a1 = da, a2 = ou, a3 = du, a4 = ov, a5 = dv;
+                    },
+                    tmin, tmax, t_out);
+                break;
+            }
+        }
+        return res;
+#elif GS_AQ_UNIFORM
+        const uint32_t c0 = __builtin_amdgcn_readfirstlane(code);
+        if (UNI || __builtin_amdgcn_ballot_w64(code != c0) == 0) {
+            switch (c0) {
+                case 0: return aquad_fixed<UNI, 0>(qs, i, Dp, ray, tmin, tmax, t_out);
+                case 1: return aquad_fixed<UNI, 1>(qs, i, Dp, ray, tmin, tmax, t_out);
+                case 2: return aquad_fixed<UNI, 2>(qs, i, Dp, ray, tmin, tmax, t_out);
+                case 3: return aquad_fixed<UNI, 3>(qs, i, Dp, ray, tmin, tmax, t_out);
+                case 4: return aquad_fixed<UNI, 4>(qs, i, Dp, ray, tmin, tmax, t_out);
+                default: return aquad_fixed<UNI, 5>(qs, i, Dp, ray, tmin, tmax, t_out);
+            }
+        }
+#endif
+        const uint32_t ax = code >> 1, o = code & 1u;
+        const uint32_t k1 = ax == 2u ? 0u : ax + 1u, k2 = ax == 0u ? 2u : ax - 1u;  // a+1, a+2 (mod 3)
+        return aquad_accept<UNI>(
+            qs, i, Dp,
+            [&](double& oa, double& da, double& ou, double& du, double& ov, double& dv) {
+                oa = d3_at(ray.o, ax);
+                da = d3_at(ray.d, ax);
+                const double o1 = d3_at(ray.o, k1), o2 = d3_at(ray.o, k2);
+                const double d1 = d3_at(ray.d, k1), d2 = d3_at(ray.d, k2);
+                ou = o ? o2 : o1;
+                ov = o ? o1 : o2;
+                du = o ? d2 : d1;
+                dv = o ? d1 : d2;
+            },
+            tmin, tmax, t_out);
+    }
+#endif
+    const u32x4 b = quad_part<UNI>(qs, i, 1);
     return quad_accept_plane(
         mk(lo_hi(a.x, a.y), lo_hi(a.z, a.w), lo_hi(b.x, b.y)), lo_hi(b.z, b.w),
         [&](d3& Q, d3& U, d3& V, d3& W) {
@@ -534,6 +668,57 @@ __device__ __forceinline__ uint32_t walk_chain(const DevScene& sc, uint32_t cur,
     return cur;
 }
 
+// A Quad::cube list (quad.rs:54-80: six quads in a fixed order, all axis-aligned, added one
+// after the other) as straight-line code: face k's plane axis and in-plane axes are
+// compile-time constants (the codes below, the aligned form's 2 a + o), so each face is
+// Quad::hit in the reduced form aquad_accept states -- the same t, alpha and beta bit for
+// bit -- with no selects and no loop, in the list's order with its shrinking closest
+// (hittable.rs:71-86).  The host (cube_record) builds a cube only when every face's record
+// has exactly that form; the other lists keep the loop.  Record: the six D' (48 B), then
+// per face Q_iu, Q_iv, U_iu, V_iv, W', 0 (48 B).
+#ifndef GS_CUBE
+#define GS_CUBE 1
+#endif
+#define GS_CUBE_FLAG 0x80000000u
+#define GS_CUBE_DOUBLES 42
+__host__ __device__ constexpr int cube_code(int k) { return k == 0 || k == 2 ? 4 : (k == 1 || k == 3 ? 1 : 3); }
+template <bool UNI>
+__device__ __forceinline__ double ld_f64(const double* p) {
+    return *sp<UNI>(p);
+}
+template <bool UNI, int K>
+__device__ __forceinline__ void cube_face(const double* cb, uint32_t q0, const Ray& r, double tmin, uint32_t inst_ref,
+                                          LeafHit& res) {
+    constexpr int C = cube_code(K);
+    const double da = d3_c<C>(r.d, 0);
+    if (fabs(da) < 1e-8) return;
+    const double t = (ld_f64<UNI>(cb + K) - d3_c<C>(r.o, 0)) / da;
+    if (!(tmin <= t && t <= res.t)) return;
+    const double* f = cb + 6 + 6 * K;
+    const double pu = (d3_c<C>(r.o, 1) + d3_c<C>(r.d, 1) * t) - ld_f64<UNI>(f + 0);
+    const double pv = (d3_c<C>(r.o, 2) + d3_c<C>(r.d, 2) * t) - ld_f64<UNI>(f + 1);
+    const double W = ld_f64<UNI>(f + 4);
+    const double alpha = W * (pu * ld_f64<UNI>(f + 3));
+    const double beta = W * (ld_f64<UNI>(f + 2) * pv);
+    if (!(0.0 <= alpha && alpha <= 1.0) || !(0.0 <= beta && beta <= 1.0)) return;
+    res.hit = true;
+    res.t = t;
+    res.ref = GS_MAKE_REF(GS_REF_QUAD, q0 + K);
+    res.inst = inst_ref;
+}
+template <bool UNI>
+__device__ __forceinline__ void cube_test(const DevScene& sc, uint32_t cube, uint32_t q0, const Ray& r, double tmin,
+                                          uint32_t inst_ref, LeafHit& res, unsigned long long* cnt) {
+    atomicAdd(&cnt[C_QUAD], 6ull);
+    const double* cb = sc.cubes + (size_t)cube * GS_CUBE_DOUBLES;
+    cube_face<UNI, 0>(cb, q0, r, tmin, inst_ref, res);
+    cube_face<UNI, 1>(cb, q0, r, tmin, inst_ref, res);
+    cube_face<UNI, 2>(cb, q0, r, tmin, inst_ref, res);
+    cube_face<UNI, 3>(cb, q0, r, tmin, inst_ref, res);
+    cube_face<UNI, 4>(cb, q0, r, tmin, inst_ref, res);
+    cube_face<UNI, 5>(cb, q0, r, tmin, inst_ref, res);
+}
+
 // A HittableList (hittable.rs:71-86: shrinking closest) or one primitive.
 // A device-side QRUN ref (DREF_QRUN, set at upload: render.hip qrun_ref) is a list whose
 // members are the quads [first, first + count) in order (every Quad::cube, quad.rs:54-80),
@@ -555,6 +740,10 @@ __device__ __forceinline__ void shape_test(const DevScene& sc, const QuadSrc& qs
             l.count = (cur & GS_REF_MASK) >> QRUN_COUNT_SHIFT;
         } else {
             l = ld_list<UNI>(sc.lists + (cur & GS_REF_MASK));
+            if (GS_CUBE && (l.count & GS_CUBE_FLAG)) {
+                cube_test<UNI>(sc, l.first, l.count & ~GS_CUBE_FLAG, r, tmin, inst_ref, res, cnt);
+                return;
+            }
         }
 #pragma unroll 1
         for (uint32_t k = 0; k < l.count; k++)
@@ -564,9 +753,13 @@ __device__ __forceinline__ void shape_test(const DevScene& sc, const QuadSrc& qs
     if ((cur >> GS_REF_SHIFT) == GS_REF_LIST) {
         atomicAdd(&cnt[C_LIST], 1ull);
         const gs_list l = ld_list<UNI>(sc.lists + (cur & GS_REF_MASK));
+        if (GS_CUBE && (l.count & GS_CUBE_FLAG)) {
+            cube_test<UNI>(sc, l.first, l.count & ~GS_CUBE_FLAG, r, tmin, inst_ref, res, cnt);
+        } else {
 #pragma unroll 1
-        for (uint32_t k = 0; k < l.count; k++)
-            prim_test<UNI>(sc, qs, ld_u32<UNI>(sc.list_refs + l.first + k), r, tmin, res.t, inst_ref, res, cnt);
+            for (uint32_t k = 0; k < l.count; k++)
+                prim_test<UNI>(sc, qs, ld_u32<UNI>(sc.list_refs + l.first + k), r, tmin, res.t, inst_ref, res, cnt);
+        }
 #endif
     } else {
         prim_test<UNI>(sc, qs, cur, r, tmin, closest, inst_ref, res, cnt);
@@ -1158,7 +1351,7 @@ __device__ __forceinline__ void count_visit(uint32_t* counts, uint32_t idx) {
 // elapsed clock to its wave's LDS slot (one count per wave, whatever the mask).
 #define GS_REGION(k, t0) do { uint64_t t1_; GS_STAMP(t1_); \
     const uint64_t em_ = __builtin_amdgcn_read_exec(); \
-    if (lane == (uint32_t)__builtin_ctzll(em_)) s_reg[(tid >> 6) * 8 + (k)] += t1_ - (t0); } while (0)
+    if (lane == (uint32_t)__builtin_ctzll(em_)) s_reg[(tid >> 6) * 16 + (k)] += t1_ - (t0); } while (0)
 #else
 #define GS_STAMP(t) do { } while (0)
 #define GS_REGION(k, t0) do { } while (0)
@@ -1185,7 +1378,7 @@ enum { L_ITEM = 0, L_PIX, L_BLEFT, L_SAMPLE, L_DEPTH, L_HINST, L_NI };  // (samp
 // LDS: the dynamic LDS then starts at address 0, so a node's LDS address is its byte
 // offset itself (node links are pre-shifted, below).
 #ifdef GS_STAMPS
-#define GS_STAMP_LDS ((GS_BLOCK / 64) * 8 * 8)
+#define GS_STAMP_LDS ((GS_BLOCK / 64) * 16 * 8)
 #else
 #define GS_STAMP_LDS 0
 #endif
@@ -1253,8 +1446,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     uint32_t* s_i = (uint32_t*)(s_d + A.lane_nd * GS_BLOCK);
     unsigned long long* s_cnt = (unsigned long long*)(s_i + lane_ni(FEAT) * GS_BLOCK);
 #ifdef GS_STAMPS
-    unsigned long long* s_reg = s_cnt + 16;  // [(GS_BLOCK / 64) * 8]
-    if (threadIdx.x < (GS_BLOCK / 64) * 8) s_reg[threadIdx.x] = 0;
+    unsigned long long* s_reg = s_cnt + 16;  // [(GS_BLOCK / 64) * 16]: shade regions 0-4, leaf kinds 8-15
+    if (threadIdx.x < (GS_BLOCK / 64) * 16) s_reg[threadIdx.x] = 0;
 #endif
     if (threadIdx.x < GS_CNT_SLOTS) s_cnt[threadIdx.x] = 0;
     __syncthreads();
@@ -1974,9 +2167,21 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                     GS_MARK("sphere_end");
                 } else if ((FEAT & GS_FEAT_SPHLEAF) != 0 || (ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {
+#ifdef GS_STAMPS
+                    uint64_t k0_;
+                    GS_STAMP(k0_);
+#endif
                     sphere_leaf();
+                    GS_REGION(7 + GS_REF_SPHERE, k0_);
                 } else if constexpr ((FEAT & GS_FEAT_SPHLEAF) == 0) {
                     GS_MARK("other_begin");
+#ifdef GS_STAMPS
+                    // (leaf-kind clock: the branch's first lane's ref kind, before any
+                    // instance chain -- one kind per pass with kind-batched leaf passes)
+                    uint64_t k0_;
+                    GS_STAMP(k0_);
+                    const uint32_t kk_ = __builtin_amdgcn_readfirstlane(ref >> GS_REF_SHIFT);
+#endif
                     // A leaf pass whose other-kind lanes all sit at one leaf (the Cornell box:
                     // always, with single node steps) tests it with scalar loads.
                     const uint32_t r0 = __builtin_amdgcn_readfirstlane(ref);
@@ -1995,6 +2200,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         hit_ref = lh.ref;
                         LI(L_HINST) = lh.inst;
                     }
+                    GS_REGION(7 + (kk_ < 1u ? 1u : kk_ > 8u ? 8u : kk_), k0_);
                     GS_MARK("other_end");
                 }
                 cur = next;
@@ -2182,7 +2388,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         atomicAdd(&dbg[7], (unsigned long long)ln_leaf);
         atomicAdd(&dbg[8], (unsigned long long)it_shade);
         atomicAdd(&dbg[9], (unsigned long long)ln_shade);
-        for (int k = 0; k < 5; k++) atomicAdd(&dbg[10 + k], s_reg[(tid >> 6) * 8 + k]);
+        for (int k = 0; k < 5; k++) atomicAdd(&dbg[10 + k], s_reg[(tid >> 6) * 16 + k]);
+        for (int k = 0; k < 8; k++) atomicAdd(&dbg[24 + k], s_reg[(tid >> 6) * 16 + 8 + k]);
         atomicAdd(&dbg[15], (unsigned long long)acc_node);
         atomicAdd(&dbg[16], (unsigned long long)acc_leaf);
         atomicAdd(&dbg[20], (unsigned long long)d_wsteps);
@@ -2610,6 +2817,69 @@ struct Placed {
 // visits per byte, which maximises the visits the mirror serves; the static estimate
 // orders the unvisited and serves when there is no pilot.  Records outside the mirror
 // stay in pre-order.
+// The aligned form of a quad's traversal record (quad_test, GS_AQUAD) when its normal is
+// exactly +-e_a, w is zero off axis a, and u, v are each non-zero on one other axis.
+static bool aligned_tquad(const gs_quad& q, TQuad& out) {
+    int ax = -1;
+    for (int k = 0; k < 3; k++) {
+        if (q.normal[k] == 0.0) continue;
+        if (std::fabs(q.normal[k]) != 1.0 || ax >= 0) return false;
+        ax = k;
+    }
+    if (ax < 0) return false;
+    auto one_axis = [&](const double* v) {
+        int at = -1;
+        for (int k = 0; k < 3; k++) {
+            if (!std::isfinite(v[k])) return -2;
+            if (v[k] != 0.0) {
+                if (at >= 0) return -2;
+                at = k;
+            }
+        }
+        return at;
+    };
+    const int iu = one_axis(q.u), iv = one_axis(q.v);
+    if (iu < 0 || iv < 0 || iu == ax || iv == ax || iu == iv) return false;
+    for (int k = 0; k < 3; k++)
+        if (k != ax && q.w[k] != 0.0) return false;
+    if (!std::isfinite(q.w[ax]) || !std::isfinite(q.d) || !std::isfinite(q.q[iu]) || !std::isfinite(q.q[iv])) return false;
+    const int o = iu == (ax + 1) % 3 ? 0 : 1;  // (then iv == (ax + 2) % 3 for o == 0)
+    const double sgn = o == 0 ? 1.0 : -1.0;
+    TQuad r{};
+    const uint64_t tag = ((uint64_t)(GS_AQ_TAG | (uint32_t)(2 * ax + o))) << 32;
+    std::memcpy(&r.nx, &tag, 8);
+    r.ny = q.normal[ax] * q.d;  // D' (exact: a sign)
+    r.nz = q.q[iu];
+    r.d = q.q[iv];
+    r.qx = q.u[iu];
+    r.qy = q.v[iv];
+    r.qz = sgn * q.w[ax];  // W'
+    out = r;
+    return true;
+}
+
+static int g_cube_lists = 1;  // gs_debug_set_cube_lists
+// A Quad::cube list's device record (cube_test): six consecutive quads whose aligned forms
+// carry cube_code(k) in order.  Returns false (the list keeps the loop) otherwise.
+static bool cube_record(const gs_flat_scene& s, const gs_list& l, uint32_t& q0, double* out) {
+    if (l.count != 6 || (uint64_t)l.first + 6 > s.n_list_refs) return false;
+    q0 = s.list_refs[l.first] & GS_REF_MASK;
+    if (q0 >= GS_CUBE_FLAG) return false;
+    for (uint32_t k = 0; k < 6; k++) {
+        const uint32_t ref = s.list_refs[l.first + k];
+        if ((ref >> GS_REF_SHIFT) != GS_REF_QUAD || (ref & GS_REF_MASK) != q0 + k || q0 + k >= s.n_quads) return false;
+        TQuad a;
+        if (!aligned_tquad(s.quads[q0 + k], a)) return false;
+        uint64_t tag;
+        std::memcpy(&tag, &a.nx, 8);
+        if ((uint32_t)(tag >> 32) != (GS_AQ_TAG | (uint32_t)cube_code((int)k))) return false;
+        out[k] = a.ny;                                       // D'
+        const double f[6] = {a.nz, a.d, a.qx, a.qy, a.qz, 0.0};  // Q_iu, Q_iv, U_iu, V_iv, W'
+        for (int j = 0; j < 6; j++) out[6 + 6 * k + j] = f[j];
+    }
+    return true;
+}
+
 static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* visits, uint32_t n_quads,
                             int64_t budget, uint32_t n_nrecs) {
     const uint32_t n = (uint32_t)t.rec.size();
@@ -2941,6 +3211,12 @@ gs_status gs_debug_set_round_items(int32_t mode) {
     return GS_OK;
 }
 
+gs_status gs_debug_set_cube_lists(int32_t on) {
+    if (on != 0 && on != 1) return fail(GS_ERR_ARG, "cube lists are 0 (the list loop) or 1 (cube_test)");
+    g_cube_lists = on;
+    return GS_OK;
+}
+
 gs_status gs_debug_set_partial_budget(uint64_t bytes) {
     g_partial_budget = bytes ? bytes : (4ull << 30);
     return GS_OK;
@@ -3196,6 +3472,11 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         const gs_quad& q = s->quads[i];
         tquads[i] = TQuad{q.normal[0], q.normal[1], q.normal[2], q.d, q.q[0], q.q[1], q.q[2], q.u[0],
                           q.u[1],      q.u[2],      q.v[0],      q.v[1], q.v[2], q.w[0], q.w[1], q.w[2]};
+        if (!(GS_AQUAD && aligned_tquad(q, tquads[i]))) {  // a full record whose first word would read as the aligned form's tag
+            uint64_t bits;
+            std::memcpy(&bits, &tquads[i].nx, 8);
+            if (((uint32_t)(bits >> 32) & ~7u) == GS_AQ_TAG) tquads[i].nx = std::nan("");  // (any NaN normal misses)
+        }
     }
     std::vector<DSphere> sph(s->n_spheres);
     std::vector<uint32_t> sph_mat(s->n_spheres);
@@ -3262,7 +3543,17 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     size_t o_msph = L.add(s->mspheres, s->n_mspheres * sizeof(gs_msphere));
     size_t o_quad = L.add(s->quads, s->n_quads * sizeof(gs_quad));
     size_t o_tri = L.add(s->triangles, s->n_triangles * sizeof(gs_triangle));
-    size_t o_list = L.add(s->lists, s->n_lists * sizeof(gs_list));
+    std::vector<gs_list> dlists(s->lists, s->lists + s->n_lists);
+    std::vector<double> cubes;
+    for (uint32_t i = 0; GS_CUBE && g_cube_lists && i < s->n_lists; i++) {
+        double rec[GS_CUBE_DOUBLES];
+        uint32_t q0;
+        if (!cube_record(*s, s->lists[i], q0, rec)) continue;
+        dlists[i] = gs_list{(uint32_t)(cubes.size() / GS_CUBE_DOUBLES), GS_CUBE_FLAG | q0};
+        cubes.insert(cubes.end(), rec, rec + GS_CUBE_DOUBLES);
+    }
+    size_t o_list = L.add(dlists.data(), dlists.size() * sizeof(gs_list));
+    size_t o_cubes = L.add(cubes.data(), cubes.size() * sizeof(double));
     size_t o_lref = L.add(s->list_refs, s->n_list_refs * 4);
     size_t o_inst = L.add(insts.data(), insts.size() * sizeof(gs_instance));
     size_t o_media = L.add(media.data(), media.size() * sizeof(gs_medium));
@@ -3301,6 +3592,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     d.tris = (const gs_triangle*)(b + o_tri);
     d.lists = (const gs_list*)(b + o_list);
     d.list_refs = (const uint32_t*)(b + o_lref);
+    d.cubes = (const double*)(b + o_cubes);
     d.inst = (const gs_instance*)(b + o_inst);
     d.media = (const gs_medium*)(b + o_media);
     d.noise_perm = (const uint8_t*)(b + o_perm);

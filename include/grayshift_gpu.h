@@ -274,6 +274,11 @@ gs_status gs_set_adaptive_mode(int32_t mode);
  * device's lanes, split after.  Every choice renders the same bits. */
 gs_status gs_debug_set_round_items(int32_t mode);
 
+/* Test hook: scenes uploaded after this call test each Quad::cube list (six consecutive
+ * axis-aligned quads in cube order) as straight-line code with the faces' axes fixed at
+ * compile time (1, default) or with the generic list loop (0).  Both render the same bits. */
+gs_status gs_debug_set_cube_lists(int32_t on);
+
 /* Test hook: the auto sample-chunk rule's budget for chunk sums (default 4 GiB; 0
  * restores it).  A smaller budget makes renders take the chunk-doubling branch. */
 gs_status gs_debug_set_partial_budget(uint64_t bytes);

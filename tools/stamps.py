@@ -49,6 +49,11 @@ def main():
     bad = int(dbg[23].item())
     if bad:
         print("WARNING: %d leaf passes whose exec mask held lanes outside the ballot (their distinct-ref / kind counts are not trusted)" % bad)
+    kinds = dbg[24:32].cpu().tolist()
+    if sum(kinds):
+        names = ["node", "sphere", "msphere", "quad", "triangle", "list", "instance", "medium"]
+        print("leaf-kind clock (%% of leaf-pass clock; a pass's non-sphere branch by its first lane's ref kind): " +
+              "  ".join("%s %.1f%%" % (n, 100.0 * x / max(1, leaf_clk)) for n, x in zip(names, kinds) if x))
     reg = dbg[10:15].cpu().tolist()
     # split shading (no GS_FEAT_MIXED) stamps background / reconstruct / scatter on their own;
     # staged shading (GS_FEAT_MIXED, media, nested) stamps all of it as region 2
