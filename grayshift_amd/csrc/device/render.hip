@@ -235,6 +235,8 @@ struct KArgs {
     uint32_t lds_quads;  // then quad records [0, lds_quads)
     uint32_t lds_nrecs;  // then the nested trees' records [0, lds_nrecs) (GS_NESTED_LDS)
     const TNode* nrecs;  // (the mirror's source)
+    uint32_t lds_cubes;  // then the Quad::cube records [0, lds_cubes) (cube_test)
+    const double* cubes; // (the mirror's source)
     uint32_t lane_nd;    // f64 lane-state fields in LDS: lane_nd(chunked)
 };
 
@@ -378,6 +380,9 @@ struct QuadSrc {
     // the nested trees' records mirrored in LDS: [0, n_nlds) at nlds (GS_NESTED_LDS)
     const uint8_t* nlds;
     uint32_t n_nlds;
+    // the Quad::cube records mirrored in LDS: [0, n_lcubes) at lcubes (cube_test)
+    const uint8_t* lcubes;
+    uint32_t n_lcubes;
 };
 
 // Scene-record loads of the leaf tests, field by field through a pointer of an explicit
@@ -668,55 +673,122 @@ __device__ __forceinline__ uint32_t walk_chain(const DevScene& sc, uint32_t cur,
     return cur;
 }
 
+// The instance tests of walking a chain again (counted, nothing computed).
+template <bool UNI>
+__device__ __forceinline__ void chain_count(const DevScene& sc, uint32_t cur, unsigned long long* cnt) {
+#pragma unroll 1
+    for (int k = 0; k < GS_MAX_CHAIN && (cur >> GS_REF_SHIFT) == GS_REF_INSTANCE; k++) {
+        atomicAdd(&cnt[C_INST], 1ull);
+        cur = ld_u32<UNI>(&sc.inst[cur & GS_REF_MASK].child);
+    }
+}
+
 // A Quad::cube list (quad.rs:54-80: six quads in a fixed order, all axis-aligned, added one
 // after the other) as straight-line code: face k's plane axis and in-plane axes are
-// compile-time constants (the codes below, the aligned form's 2 a + o), so each face is
-// Quad::hit in the reduced form aquad_accept states -- the same t, alpha and beta bit for
-// bit -- with no selects and no loop, in the list's order with its shrinking closest
-// (hittable.rs:71-86).  The host (cube_record) builds a cube only when every face's record
-// has exactly that form; the other lists keep the loop.  Record: the six D' (48 B), then
-// per face Q_iu, Q_iv, U_iu, V_iv, W', 0 (48 B).
+// compile-time constants (cube_code: the aligned form's 2 a + o), so each face is Quad::hit
+// in the reduced form aquad_accept states -- the same t, alpha and beta bit for bit -- with
+// no selects and no loop, in the list's order with its shrinking closest (hittable.rs:
+// 71-86).  Every face value is one of twelve numbers of the box: its corners min = (x0, y0,
+// z0) and max = (x1, y1, z1), the edges dx, dy, dz and the three w magnitudes (w_xy of the
+// z faces, w_zy of the x faces, w_xz of the y faces), with a sign: the 96-B record
+// [x0 y0 z0 x1 y1 z1 dx dy dz w_xy w_zy w_xz] (a negation is exact and free, an f64
+// operand modifier).  The host (cube_record) builds a cube only when all six faces' aligned
+// records equal what this table derives; the other lists keep the loop.
 #ifndef GS_CUBE
 #define GS_CUBE 1
 #endif
+#ifndef GS_CUBE_LDS
+#define GS_CUBE_LDS 1  // mirror a prefix of the cube records in LDS (after the other mirrors)
+#endif
 #define GS_CUBE_FLAG 0x80000000u
-#define GS_CUBE_DOUBLES 42
+#define GS_CUBE_DOUBLES 12
 __host__ __device__ constexpr int cube_code(int k) { return k == 0 || k == 2 ? 4 : (k == 1 || k == 3 ? 1 : 3); }
-template <bool UNI>
-__device__ __forceinline__ double ld_f64(const double* p) {
-    return *sp<UNI>(p);
+// face k's D', Q_iu, Q_iv, U_iu, V_iv, W' as (record index, sign): quad.rs:73-78 in order
+__host__ __device__ constexpr int cube_src(int k, int f) {
+    constexpr int t[6][6] = {{5, 0, 1, 6, 7, 9},    {3, 5, 1, -8, 7, -10}, {2, 3, 1, -6, 7, -9},
+                             {0, 2, 1, 8, 7, 10},   {4, 0, 5, 6, -8, -11}, {1, 0, 2, 6, 8, 11}};
+    return t[k][f];
 }
-template <bool UNI, int K>
-__device__ __forceinline__ void cube_face(const double* cb, uint32_t q0, const Ray& r, double tmin, uint32_t inst_ref,
+#ifndef GS_CUBE_LAZY
+#define GS_CUBE_LAZY 0  // 1: each face reads the values it needs when it needs them; 0: all 12 first
+#endif
+struct CubeRegs {  // the record read up front
+    double c[GS_CUBE_DOUBLES];
+    template <int J>
+    __device__ __forceinline__ double get() const { return c[J]; }
+};
+template <bool UNI>
+struct CubeLazy {  // the record where it lies: the LDS mirror or global memory
+    const uint8_t* lds;
+    const double* g;
+    bool in_lds;
+    template <int J>
+    __device__ __forceinline__ double get() const {
+        if (!UNI && in_lds) return *(const __attribute__((address_space(3))) double*)(uintptr_t)(lds + 8 * J);
+        return *sp<UNI>(g + J);
+    }
+};
+template <bool UNI>
+__device__ __forceinline__ u32x4 cube_part(const QuadSrc& qs, const double* g, uint32_t cube, uint32_t k, bool lds) {
+    if (!UNI && lds) return *(lds_u32x4*)(qs.lcubes + cube * (uint32_t)(GS_CUBE_DOUBLES * 8) + (k << 4));
+    return sp<UNI>(reinterpret_cast<const u32x4*>(g + (size_t)cube * GS_CUBE_DOUBLES))[k];
+}
+template <int K, int F, class Src>
+__device__ __forceinline__ double cube_val(const Src& c) {
+    constexpr int v = cube_src(K, F);
+    if constexpr (v < 0) return -c.template get<-v>();
+    else return c.template get<v>();
+}
+template <int K, class Src>
+__device__ __forceinline__ void cube_face(const Src& c, uint32_t q0, const Ray& r, double tmin, uint32_t inst_ref,
                                           LeafHit& res) {
     constexpr int C = cube_code(K);
     const double da = d3_c<C>(r.d, 0);
     if (fabs(da) < 1e-8) return;
-    const double t = (ld_f64<UNI>(cb + K) - d3_c<C>(r.o, 0)) / da;
+    const double t = (cube_val<K, 0>(c) - d3_c<C>(r.o, 0)) / da;
     if (!(tmin <= t && t <= res.t)) return;
-    const double* f = cb + 6 + 6 * K;
-    const double pu = (d3_c<C>(r.o, 1) + d3_c<C>(r.d, 1) * t) - ld_f64<UNI>(f + 0);
-    const double pv = (d3_c<C>(r.o, 2) + d3_c<C>(r.d, 2) * t) - ld_f64<UNI>(f + 1);
-    const double W = ld_f64<UNI>(f + 4);
-    const double alpha = W * (pu * ld_f64<UNI>(f + 3));
-    const double beta = W * (ld_f64<UNI>(f + 2) * pv);
+    const double pu = (d3_c<C>(r.o, 1) + d3_c<C>(r.d, 1) * t) - cube_val<K, 1>(c);
+    const double pv = (d3_c<C>(r.o, 2) + d3_c<C>(r.d, 2) * t) - cube_val<K, 2>(c);
+    const double W = cube_val<K, 5>(c);
+    const double alpha = W * (pu * cube_val<K, 4>(c));
+    const double beta = W * (cube_val<K, 3>(c) * pv);
     if (!(0.0 <= alpha && alpha <= 1.0) || !(0.0 <= beta && beta <= 1.0)) return;
     res.hit = true;
     res.t = t;
     res.ref = GS_MAKE_REF(GS_REF_QUAD, q0 + K);
     res.inst = inst_ref;
 }
+template <class Src>
+__device__ __forceinline__ void cube_faces(const Src& c, uint32_t q0, const Ray& r, double tmin, uint32_t inst_ref,
+                                           LeafHit& res) {
+    cube_face<0>(c, q0, r, tmin, inst_ref, res);
+    cube_face<1>(c, q0, r, tmin, inst_ref, res);
+    cube_face<2>(c, q0, r, tmin, inst_ref, res);
+    cube_face<3>(c, q0, r, tmin, inst_ref, res);
+    cube_face<4>(c, q0, r, tmin, inst_ref, res);
+    cube_face<5>(c, q0, r, tmin, inst_ref, res);
+}
 template <bool UNI>
-__device__ __forceinline__ void cube_test(const DevScene& sc, uint32_t cube, uint32_t q0, const Ray& r, double tmin,
-                                          uint32_t inst_ref, LeafHit& res, unsigned long long* cnt) {
+__device__ __forceinline__ void cube_test(const DevScene& sc, const QuadSrc& qs, uint32_t cube, uint32_t q0,
+                                          const Ray& r, double tmin, uint32_t inst_ref, LeafHit& res,
+                                          unsigned long long* cnt) {
     atomicAdd(&cnt[C_QUAD], 6ull);
-    const double* cb = sc.cubes + (size_t)cube * GS_CUBE_DOUBLES;
-    cube_face<UNI, 0>(cb, q0, r, tmin, inst_ref, res);
-    cube_face<UNI, 1>(cb, q0, r, tmin, inst_ref, res);
-    cube_face<UNI, 2>(cb, q0, r, tmin, inst_ref, res);
-    cube_face<UNI, 3>(cb, q0, r, tmin, inst_ref, res);
-    cube_face<UNI, 4>(cb, q0, r, tmin, inst_ref, res);
-    cube_face<UNI, 5>(cb, q0, r, tmin, inst_ref, res);
+#if GS_CUBE_LAZY
+    const CubeLazy<UNI> c{qs.lcubes + cube * (uint32_t)(GS_CUBE_DOUBLES * 8), sc.cubes + (size_t)cube * GS_CUBE_DOUBLES,
+                          cube < qs.n_lcubes};
+#else
+    CubeRegs c;
+    // the LDS copy when every lane's cube is mirrored (a wave-uniform choice: a per-lane
+    // one ran both kinds of loads under masks, final_scene -2.3%), else global for all
+    const bool lds = !UNI && __builtin_amdgcn_ballot_w64(cube >= qs.n_lcubes) == 0;
+#pragma unroll
+    for (uint32_t k = 0; k < GS_CUBE_DOUBLES / 2; k++) {
+        const u32x4 v = cube_part<UNI>(qs, sc.cubes, cube, k, lds);
+        c.c[2 * k] = lo_hi(v.x, v.y);
+        c.c[2 * k + 1] = lo_hi(v.z, v.w);
+    }
+#endif
+    cube_faces(c, q0, r, tmin, inst_ref, res);
 }
 
 // A HittableList (hittable.rs:71-86: shrinking closest) or one primitive.
@@ -741,7 +813,7 @@ __device__ __forceinline__ void shape_test(const DevScene& sc, const QuadSrc& qs
         } else {
             l = ld_list<UNI>(sc.lists + (cur & GS_REF_MASK));
             if (GS_CUBE && (l.count & GS_CUBE_FLAG)) {
-                cube_test<UNI>(sc, l.first, l.count & ~GS_CUBE_FLAG, r, tmin, inst_ref, res, cnt);
+                cube_test<UNI>(sc, qs, l.first, l.count & ~GS_CUBE_FLAG, r, tmin, inst_ref, res, cnt);
                 return;
             }
         }
@@ -754,7 +826,7 @@ __device__ __forceinline__ void shape_test(const DevScene& sc, const QuadSrc& qs
         atomicAdd(&cnt[C_LIST], 1ull);
         const gs_list l = ld_list<UNI>(sc.lists + (cur & GS_REF_MASK));
         if (GS_CUBE && (l.count & GS_CUBE_FLAG)) {
-            cube_test<UNI>(sc, l.first, l.count & ~GS_CUBE_FLAG, r, tmin, inst_ref, res, cnt);
+            cube_test<UNI>(sc, qs, l.first, l.count & ~GS_CUBE_FLAG, r, tmin, inst_ref, res, cnt);
         } else {
 #pragma unroll 1
             for (uint32_t k = 0; k < l.count; k++)
@@ -769,7 +841,7 @@ __device__ __forceinline__ void shape_test(const DevScene& sc, const QuadSrc& qs
 // ConstantMedium::hit (volume.rs:32-63): the boundary hit over Interval::UNIVERSE, again
 // from t1 + 0.0001, both clipped to ray_t; then the free-flight distance from the lane's
 // RNG stream, drawn here, inside traversal, in the reference's visit order (:48).
-template <bool UNI>
+template <bool UNI, bool REUSE>
 __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& qs, uint32_t cur, const Ray& r, double tmin,
                                             double closest, uint32_t inst_ref, uint64_t& rng, LeafHit& res,
                                             unsigned long long* cnt) {
@@ -780,6 +852,15 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
         uint32_t boundary;
     } md{ld_u32<UNI>(&mp->boundary)};
     const double DMAX = 1.7976931348623157e308;  // f64::MAX; f64::MIN = -f64::MAX
+    // REUSE: |ray.d| now (the same value volume.rs:55 computes at the end), so the ray itself
+    // is not live through the boundary tests: they need only its transform into the
+    // boundary's space, which the second boundary.hit call (volume.rs:38-41) would recompute
+    // from the same ray bit for bit -- it is reused, and the second walk's instance tests
+    // are counted.  (Media-only kernels: without it they spill 12-20 B/lane around the cube
+    // tests of box boundaries; media + nested-BVH kernels keep the second walk, with which
+    // they have the registers.)
+    double ray_len = 0.0;
+    if constexpr (REUSE) ray_len = sqrt(len2(r.d));
     LeafHit b1;
     b1.hit = false;
     b1.t = DMAX;
@@ -787,11 +868,15 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
     const uint32_t shape = walk_chain<UNI>(sc, md.boundary, rb, cnt);
     shape_test<UNI, false>(sc, qs, shape, rb, -DMAX, DMAX, GS_REF_NONE, b1, cnt);
     if (!b1.hit) return;
+    if constexpr (REUSE) {
+        chain_count<UNI>(sc, md.boundary, cnt);
+    } else {
+        rb = r;
+        walk_chain<UNI>(sc, md.boundary, rb, cnt);
+    }
     LeafHit b2;
     b2.hit = false;
     b2.t = DMAX;
-    rb = r;
-    walk_chain<UNI>(sc, md.boundary, rb, cnt);  // the second boundary.hit call walks the chain again
     shape_test<UNI, false>(sc, qs, shape, rb, b1.t + 0.0001, DMAX, GS_REF_NONE, b2, cnt);
     if (!b2.hit) return;
     double t1 = b1.t, t2 = b2.t;
@@ -799,7 +884,7 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
     if (t2 > closest) t2 = closest;
     if (t1 >= t2) return;
     if (t1 < 0.0) t1 = 0.0;
-    const double ray_len = sqrt(len2(r.d));
+    if constexpr (!REUSE) ray_len = sqrt(len2(r.d));
     const double dist_inside_boundary = (t2 - t1) * ray_len;
     const double hit_dist = sp<UNI>(mp)->density_neg_inv * log(wy_f64(rng));
     if (hit_dist > dist_inside_boundary) return;
@@ -821,6 +906,9 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
 // cert ray (round 3: half the bytes per node and fewer registers than the f64 walk).
 // `root`: the tree's first record.  Leaves are lists or primitives (validated).
 #define NREC_LEAF 0x80000000u
+#ifndef GS_NESTED_WW
+#define GS_NESTED_WW 0  // 1: measured neutral on final_scene (2 142 vs 2 155, profiles/r04/ab_cube_records.txt)
+#endif
 __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs, uint32_t root, const Ray& r, double tmin,
                                            double closest, uint32_t inst_ref, LeafHit& res,
                                            unsigned long long* cnt) {
@@ -834,6 +922,48 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
     }
     float closest32 = (float)closest;
     uint32_t cur = root;
+#if GS_NESTED_WW
+    // "while-while": node steps until every lane of the walk sits at a leaf or has ended,
+    // then the leaf lanes test their leaves together (a sphere test costs several node
+    // steps: with one loop, an iteration whose lanes were at both kinds paid for both).
+    // Each lane's records, order and results are those of the single loop.
+#pragma unroll 1
+    while (cur != THR_END) {
+        u32x4 a, b;
+#pragma unroll 1
+        for (;;) {
+            // (a scalar branch to the LDS reads when every active lane's record is mirrored)
+            if (__builtin_amdgcn_ballot_w64(cur >= qs.n_nlds) == 0) {
+                a = *(lds_u32x4*)(qs.nlds + cur * 32u);
+                b = *(lds_u32x4*)(qs.nlds + cur * 32u + 16u);
+            } else {
+                const u32x4* q = sp<false>(reinterpret_cast<const u32x4*>(sc.nrecs + cur));
+                a = q[0];
+                b = q[1];
+            }
+            if (b.z & NREC_LEAF) break;
+            atomicAdd(&cnt[C_NODES], 1ull);
+            bool h = false, undecided = true;
+            if (fast)
+                h = box_cert(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(b.x), __uint_as_float(a.z),
+                             __uint_as_float(a.w), __uint_as_float(b.y), c, 0.001f, closest32, undecided);
+            if (undecided) h = box_hit_v(ld_node_g(sc.nodes + cur), r.o, inv_of(r.d), tmin, closest);
+#ifdef GS_CERT_CHECK
+            if (fast && !undecided && box_hit_v(ld_node_g(sc.nodes + cur), r.o, inv_of(r.d), tmin, closest) != h)
+                atomicAdd(&cnt[15], 1ull);
+#endif
+            cur = h ? b.z : b.w;
+            if (cur == THR_END) break;
+        }
+        if (cur == THR_END) break;
+        shape_test<false>(sc, qs, b.w, r, tmin, closest, inst_ref, res, cnt);
+        if (res.hit) {  // res.t only ever shrinks
+            closest = res.t;
+            closest32 = (float)res.t;
+        }
+        cur = b.z & ~NREC_LEAF;
+    }
+#else
 #pragma unroll 1
     while (cur != THR_END) {
         u32x4 a, b;
@@ -869,6 +999,7 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
             cur = h ? b.z : b.w;
         }
     }
+#endif
 }
 
 // The rarer non-node children (everything but a stationary sphere reached directly
@@ -888,7 +1019,7 @@ __device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, const QuadSrc& qs,
     const uint32_t inst_ref = (ref >> GS_REF_SHIFT) == GS_REF_INSTANCE ? ref : GS_REF_NONE;
     const uint32_t cur = walk_chain<UNI>(sc, ref, r, cnt);
     if ((FEAT & GS_FEAT_MEDIA) && (cur >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
-        medium_test<UNI>(sc, qs, cur, r, tmin, closest, inst_ref, rng, res, cnt);
+        medium_test<UNI, (FEAT & GS_FEAT_NESTED) == 0>(sc, qs, cur, r, tmin, closest, inst_ref, rng, res, cnt);
     } else if ((FEAT & GS_FEAT_NESTED) && (cur >> GS_REF_SHIFT) == GS_REF_NODE) {
         nested_bvh(sc, qs, cur & GS_REF_MASK, r, tmin, closest, inst_ref, res, cnt);
     } else {
@@ -1438,11 +1569,15 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             dst = reinterpret_cast<uint4*>(s_quads + (size_t)A.lds_quads * sizeof(TQuad));
             for (uint32_t k = threadIdx.x; k < A.lds_nrecs * 2u; k += GS_BLOCK) dst[k] = src[k];
         }
+        src = reinterpret_cast<const uint4*>(A.cubes);
+        dst = reinterpret_cast<uint4*>(s_quads + (size_t)A.lds_quads * sizeof(TQuad) + (size_t)A.lds_nrecs * sizeof(TNode));
+        for (uint32_t k = threadIdx.x; k < A.lds_cubes * (GS_CUBE_DOUBLES / 2); k += GS_BLOCK) dst[k] = src[k];
     }
     uint8_t* s_nrecs = s_quads + (size_t)A.lds_quads * sizeof(TQuad);
-    const QuadSrc qs{s_quads, A.tquads, A.lds_quads, s_nrecs, A.lds_nrecs};
+    uint8_t* s_cubes = s_nrecs + (size_t)A.lds_nrecs * sizeof(TNode);
+    const QuadSrc qs{s_quads, A.tquads, A.lds_quads, s_nrecs, A.lds_nrecs, s_cubes, A.lds_cubes};
     // Per-lane pixel / path state after the mirror: [L_ND][GS_BLOCK] f64, [L_NI][GS_BLOCK] u32.
-    double* s_d = (double*)(s_nrecs + (size_t)A.lds_nrecs * sizeof(TNode));
+    double* s_d = (double*)(s_cubes + (size_t)A.lds_cubes * (GS_CUBE_DOUBLES * 8));
     uint32_t* s_i = (uint32_t*)(s_d + A.lane_nd * GS_BLOCK);
     unsigned long long* s_cnt = (unsigned long long*)(s_i + lane_ni(FEAT) * GS_BLOCK);
 #ifdef GS_STAMPS
@@ -2756,6 +2891,7 @@ struct gs_device_scene {
     uint32_t thr_root = THR_END;
     uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0;  // mirrored prefixes (per block)
     uint32_t n_nrecs = 0, lds_nrecs = 0;  // nested trees' records, and the mirrored prefix of them
+    uint32_t n_cubes = 0, lds_cubes = 0;  // Quad::cube records (cube_test), and the mirrored prefix
     const TNode* nrecs = nullptr;
     int32_t node_steps = GS_NODE_STEPS;      // node steps per node pass (from the tree's shape)
     int32_t leaf_batch = 12;                 // lanes at a leaf before a leaf pass (scene's choice)
@@ -2769,7 +2905,7 @@ struct gs_device_scene {
     // instantiation (feat minus GS_FEAT_LDSTREE when the mirror is a strict prefix), blocks/CU.
     struct LaunchCfg {
         bool ready = false;
-        uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_nrecs = 0;
+        uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_nrecs = 0, lds_cubes = 0;
         size_t lds = 0;
         int feat = 0, per_cu = 0;
     } lcfg[2];
@@ -2781,6 +2917,7 @@ struct gs_device_scene {
     ThreadedTree tree;
     std::vector<uint32_t> pos;  // tree record -> position (current placement)
     uint32_t n_quads = 0;
+    std::vector<uint32_t> single_quads;  // the quads outside cube lists (place_records)
     int64_t mirror_budget = 0;
     std::atomic<int> placement{0};  // 0 static, pilot pending; 1 static (final); 2 measured
     double pilot_ms = 0.0;
@@ -2806,7 +2943,7 @@ struct Placed {
     std::vector<TBox> tboxes;
     std::vector<TLeaf> tleaves;
     std::vector<uint32_t> pos;  // tree record -> its position in tnodes / tleaves
-    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_nrecs = 0, root = THR_END;
+    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_nrecs = 0, lds_cubes = 0, root = THR_END;
 };
 #ifndef GS_LDS_LEAVES
 #define GS_LDS_LEAVES 1  // 0: mirror node records only
@@ -2860,11 +2997,13 @@ static bool aligned_tquad(const gs_quad& q, TQuad& out) {
 
 static int g_cube_lists = 1;  // gs_debug_set_cube_lists
 // A Quad::cube list's device record (cube_test): six consecutive quads whose aligned forms
-// carry cube_code(k) in order.  Returns false (the list keeps the loop) otherwise.
+// carry cube_code(k) in order and equal, field by field, what cube_src derives from the 12
+// numbers taken from them.  Returns false (the list keeps the loop) otherwise.
 static bool cube_record(const gs_flat_scene& s, const gs_list& l, uint32_t& q0, double* out) {
     if (l.count != 6 || (uint64_t)l.first + 6 > s.n_list_refs) return false;
     q0 = s.list_refs[l.first] & GS_REF_MASK;
     if (q0 >= GS_CUBE_FLAG) return false;
+    double f[6][6];  // face k: D', Q_iu, Q_iv, U_iu, V_iv, W'
     for (uint32_t k = 0; k < 6; k++) {
         const uint32_t ref = s.list_refs[l.first + k];
         if ((ref >> GS_REF_SHIFT) != GS_REF_QUAD || (ref & GS_REF_MASK) != q0 + k || q0 + k >= s.n_quads) return false;
@@ -2873,15 +3012,24 @@ static bool cube_record(const gs_flat_scene& s, const gs_list& l, uint32_t& q0, 
         uint64_t tag;
         std::memcpy(&tag, &a.nx, 8);
         if ((uint32_t)(tag >> 32) != (GS_AQ_TAG | (uint32_t)cube_code((int)k))) return false;
-        out[k] = a.ny;                                       // D'
-        const double f[6] = {a.nz, a.d, a.qx, a.qy, a.qz, 0.0};  // Q_iu, Q_iv, U_iu, V_iv, W'
-        for (int j = 0; j < 6; j++) out[6 + 6 * k + j] = f[j];
+        const double v[6] = {a.ny, a.nz, a.d, a.qx, a.qy, a.qz};
+        for (int j = 0; j < 6; j++) f[k][j] = v[j];
     }
+    // x0 y0 z0 x1 y1 z1 dx dy dz w_xy w_zy w_xz, read off faces 3, 5, 2, 1, 4, 0 (cube_src)
+    const double c[GS_CUBE_DOUBLES] = {f[3][0], f[5][0], f[2][0], f[1][0], f[4][0], f[0][0],
+                                       f[0][3], f[0][4], f[3][3], f[0][5], f[3][5], f[5][5]};
+    for (int k = 0; k < 6; k++)
+        for (int j = 0; j < 6; j++) {
+            const int v = cube_src(k, j);
+            if (!(f[k][j] == (v < 0 ? -c[-v] : c[v]))) return false;
+        }
+    for (int j = 0; j < GS_CUBE_DOUBLES; j++) out[j] = c[j];
     return true;
 }
 
-static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* visits, uint32_t n_quads,
-                            int64_t budget, uint32_t n_nrecs) {
+static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* visits,
+                            const std::vector<uint32_t>& single_quads, int64_t budget, uint32_t n_nrecs,
+                            uint32_t n_cubes) {
     const uint32_t n = (uint32_t)t.rec.size();
     Placed out;
     std::vector<uint32_t> order(n), pos(n);
@@ -2920,7 +3068,15 @@ static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* 
                                                                         (int64_t)sizeof(TNode))
                                   : 0u;
     used += (int64_t)out.lds_nrecs * (int64_t)sizeof(TNode);
-    out.lds_quads = (uint32_t)std::min<int64_t>(n_quads, std::max<int64_t>(0, budget - used) / (int64_t)sizeof(TQuad));
+    // a prefix of the quads up to the last quad tested by the quad test that fits (cube-list
+    // quads are read from the cube records)
+    const int64_t fit = std::max<int64_t>(0, budget - used) / (int64_t)sizeof(TQuad);
+    out.lds_quads = 0;
+    for (uint32_t q : single_quads)
+        if ((int64_t)q < fit) out.lds_quads = q + 1;
+    used += (int64_t)out.lds_quads * (int64_t)sizeof(TQuad);
+    // then the Quad::cube records (cube order)
+    out.lds_cubes = GS_CUBE_LDS ? (uint32_t)std::min<int64_t>(n_cubes, std::max<int64_t>(0, budget - used) / (GS_CUBE_DOUBLES * 8)) : 0u;
     // The mirrored records take their positions in rank order, so a launch that must
     // shrink the prefixes (a larger lane state, gs_render_tiles_timed_async) drops the
     // least-tested ones; the rest keep pre-order.
@@ -3233,6 +3389,26 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GS_ERR_NO_DEVICE, "no HIP device visible");
 
+    // Quad::cube lists (cube_test): their device list records and cube records.  Their quads
+    // are never read through the quad mirror, so the mirror holds a prefix of the quads only
+    // as far as the last other quad in it (mirror_quads).
+    std::vector<gs_list> dlists(s->lists, s->lists + s->n_lists);
+    std::vector<double> cubes;
+    std::vector<uint8_t> in_cube(s->n_quads, 0);
+    for (uint32_t i = 0; GS_CUBE && g_cube_lists && i < s->n_lists; i++) {
+        double rec[GS_CUBE_DOUBLES];
+        uint32_t q0;
+        if (!cube_record(*s, s->lists[i], q0, rec)) continue;
+        dlists[i] = gs_list{(uint32_t)(cubes.size() / GS_CUBE_DOUBLES), GS_CUBE_FLAG | q0};
+        cubes.insert(cubes.end(), rec, rec + GS_CUBE_DOUBLES);
+        for (uint32_t k = 0; k < 6; k++) in_cube[q0 + k] = 1;
+    }
+    // (a quad may also be referenced directly elsewhere: any ref outside a cube list keeps
+    // it a mirror candidate -- conservatively, every quad not in a cube list)
+    std::vector<uint32_t> single_quads;
+    for (uint32_t i = 0; i < s->n_quads; i++)
+        if (!in_cube[i]) single_quads.push_back(i);
+
     // BVHs under instance chains (nested_bvh): each distinct root threaded once into
     // `nodes` (pre-order records: node {box, hit = next record, miss = after its subtree,
     // pad0 = 0}, leaf {next, ABI ref, pad0 = 1}; THR_END ends a tree), and the device copy
@@ -3339,7 +3515,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     std::vector<TNode> tnodes;
     std::vector<TBox> tboxes;
     std::vector<TLeaf> tleaves;
-    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_nrecs = 0, thr_root_tagged = THR_END;
+    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_nrecs = 0, lds_cubes = 0, thr_root_tagged = THR_END;
     ThreadedTree tree_keep;  // kept by the scene: re-placed after a launch's pilot (place_records)
     std::vector<uint32_t> placed_pos;
     double nodes_per_leaf = 0.0, other_leaf_frac = 0.0;
@@ -3430,8 +3606,9 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             }
         }
         tree_keep = ThreadedTree{thr, thr_leaf, std::move(depth), std::move(score)};
-        const Placed pl = place_records(tree_keep, nullptr, s->n_quads,
-                                        g_lds_mirror < 0 ? lds_mirror_budget() : g_lds_mirror, (uint32_t)nrecs.size());
+        const Placed pl = place_records(tree_keep, nullptr, single_quads,
+                                        g_lds_mirror < 0 ? lds_mirror_budget() : g_lds_mirror, (uint32_t)nrecs.size(),
+                                        (uint32_t)(cubes.size() / GS_CUBE_DOUBLES));
         tnodes = pl.tnodes;
         tboxes = pl.tboxes;
         tleaves = pl.tleaves;
@@ -3439,6 +3616,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         lds_leaves = pl.lds_leaves;
         lds_quads = pl.lds_quads;
         lds_nrecs = pl.lds_nrecs;
+        lds_cubes = pl.lds_cubes;
         thr_root_tagged = pl.root;
         placed_pos = pl.pos;
         // Leaf runs pay when at least a quarter of the leaf records are the first of two
@@ -3543,15 +3721,6 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     size_t o_msph = L.add(s->mspheres, s->n_mspheres * sizeof(gs_msphere));
     size_t o_quad = L.add(s->quads, s->n_quads * sizeof(gs_quad));
     size_t o_tri = L.add(s->triangles, s->n_triangles * sizeof(gs_triangle));
-    std::vector<gs_list> dlists(s->lists, s->lists + s->n_lists);
-    std::vector<double> cubes;
-    for (uint32_t i = 0; GS_CUBE && g_cube_lists && i < s->n_lists; i++) {
-        double rec[GS_CUBE_DOUBLES];
-        uint32_t q0;
-        if (!cube_record(*s, s->lists[i], q0, rec)) continue;
-        dlists[i] = gs_list{(uint32_t)(cubes.size() / GS_CUBE_DOUBLES), GS_CUBE_FLAG | q0};
-        cubes.insert(cubes.end(), rec, rec + GS_CUBE_DOUBLES);
-    }
     size_t o_list = L.add(dlists.data(), dlists.size() * sizeof(gs_list));
     size_t o_cubes = L.add(cubes.data(), cubes.size() * sizeof(double));
     size_t o_lref = L.add(s->list_refs, s->n_list_refs * 4);
@@ -3623,6 +3792,9 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ds->lds_quads = lds_quads;
     ds->lds_nrecs = lds_nrecs;
     ds->n_nrecs = (uint32_t)nrecs.size();
+    ds->single_quads = single_quads;
+    ds->lds_cubes = lds_cubes;
+    ds->n_cubes = (uint32_t)(cubes.size() / GS_CUBE_DOUBLES);
     ds->nrecs = (const TNode*)(b + o_nrecs);
     ds->node_records = (uint32_t)tnodes.size();
     ds->leaf_records = (uint32_t)tleaves.size();
@@ -3946,12 +4118,14 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         if (fa.sharedSizeBytes != 0) return fail(GS_ERR_UNSUPPORTED, "render kernel with static LDS");
         const int64_t room = (int64_t)max_lds - (int64_t)lane_lds_bytes(chunked, ds->feat);
         if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
-        uint32_t ln = ds->lds_nodes, ll = ds->lds_leaves, lq = ds->lds_quads, lr = ds->lds_nrecs;
+        uint32_t ln = ds->lds_nodes, ll = ds->lds_leaves, lq = ds->lds_quads, lr = ds->lds_nrecs, lk = ds->lds_cubes;
         auto bytes = [&] {
             return (int64_t)ln * (int64_t)sizeof(TNode) + (int64_t)ll * (int64_t)sizeof(TLeaf) +
-                   (int64_t)lq * (int64_t)sizeof(TQuad) + (int64_t)lr * (int64_t)sizeof(TNode);
+                   (int64_t)lq * (int64_t)sizeof(TQuad) + (int64_t)lr * (int64_t)sizeof(TNode) +
+                   (int64_t)lk * (GS_CUBE_DOUBLES * 8);
         };
-        // shrink the least valuable prefix first: quads, then nested records, then all
+        // shrink the least valuable prefix first: cubes, quads, then nested records, then all
+        while (bytes() > room && lk) lk = lk - 1 - lk / 16;
         while (bytes() > room && lq) lq = lq - 1 - lq / 16;
         while (bytes() > room && lr) lr = lr - 1 - lr / 16;
         while (bytes() > room) {
@@ -3962,6 +4136,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         lc.lds_leaves = ll;
         lc.lds_quads = lq;
         lc.lds_nrecs = (ds->feat & GS_FEAT_NESTED) ? lr : 0u;
+        lc.lds_cubes = lk;
         lc.lds = lane_lds_bytes(chunked, ds->feat) + (size_t)bytes();
         lc.feat = ds->feat;
         if (ln < ds->node_records || ll < ds->leaf_records) lc.feat &= ~GS_FEAT_LDSTREE;
@@ -3977,6 +4152,8 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     a.lds_quads = lc.lds_quads;
     a.lds_nrecs = lc.lds_nrecs;
     a.nrecs = ds->nrecs;
+    a.lds_cubes = lc.lds_cubes;
+    a.cubes = ds->dev.cubes;
     a.lane_nd = lane_nd(chunked, ds->feat);
     const int per_cu = g_blocks_per_cu > 0 ? g_blocks_per_cu : lc.per_cu;
     int64_t blocks = (int64_t)cus * per_cu;
@@ -4186,7 +4363,7 @@ static gs_status pilot_end(gs_device_scene* ds, PilotRun& pr) {
     const ThreadedTree& t = ds->tree;
     std::vector<uint64_t> counts(t.rec.size());
     for (size_t i = 0; i < t.rec.size(); i++) counts[i] = t.leaf[i] ? vis[(size_t)nn + ds->pos[i]] : vis[ds->pos[i]];
-    Placed pl = place_records(t, &counts, ds->n_quads, ds->mirror_budget, ds->n_nrecs);
+    Placed pl = place_records(t, &counts, ds->single_quads, ds->mirror_budget, ds->n_nrecs, ds->n_cubes);
     if (pl.tnodes.size() != nn || pl.tleaves.size() != nl) return fail(GS_ERR_HIP, "placement changed the record counts");
     // Nothing of this scene runs on the device yet (the pilot was its first launch and has
     // finished), so the arrays are rewritten in place.
@@ -4201,6 +4378,7 @@ static gs_status pilot_end(gs_device_scene* ds, PilotRun& pr) {
         ds->lds_leaves = pl.lds_leaves;
         ds->lds_quads = pl.lds_quads;
         ds->lds_nrecs = pl.lds_nrecs;
+        ds->lds_cubes = pl.lds_cubes;
         ds->pos = std::move(pl.pos);
         ds->lcfg[0].ready = ds->lcfg[1].ready = false;  // mirror prefixes changed
     }
