@@ -92,6 +92,11 @@ using namespace gsd;
 #define GS_FEAT_VISITS 32 // count tests per threaded record (the placement pilot, run_pilot)
 #define GS_FEAT_SPHLEAF 64 // every top-level leaf is a stationary sphere (no media / nested BVHs):
                            // leaf passes without the other kinds' code or the kind test
+#ifndef GS_NSPH
+#define GS_NSPH 1
+#endif
+#define GS_FEAT_NSPH 128   // with GS_FEAT_NESTED: every nested leaf is a stationary sphere
+                           // (nested_leaf without the kind dispatch)
 // The pilot's instantiation: every code path (any scene), plus the counts.
 #define GS_FEAT_PILOT (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_VISITS)
 
@@ -906,9 +911,31 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
 // cert ray (round 3: half the bytes per node and fewer registers than the f64 walk).
 // `root`: the tree's first record.  Leaves are lists or primitives (validated).
 #define NREC_LEAF 0x80000000u
+// A nested leaf: in kernels for scenes whose nested leaves are all stationary spheres (the
+// box of balls, main.rs:741-755; GS_FEAT_NSPH), Sphere::hit directly, with no kind
+// dispatch; else the generic test.  (A runtime branch between the two, and |d|^2 hoisted
+// out of the walk, spilled 8-16 B/lane.)
+template <bool SPH>
+__device__ __forceinline__ void nested_leaf(const DevScene& sc, const QuadSrc& qs, uint32_t ref, const Ray& r, double tmin, double closest, uint32_t inst_ref, LeafHit& res,
+                                            unsigned long long* cnt) {
+    if constexpr (SPH) {
+        atomicAdd(&cnt[C_SPH], 1ull);
+        const auto sp_ = sp<false>(sc.spheres + (ref & GS_REF_MASK));
+        double t;
+        if (sphere_accept(mk(sp_->cx, sp_->cy, sp_->cz), sp_->r, r, len2(r.d), tmin, closest, t)) {
+            res.hit = true;
+            res.t = t;
+            res.ref = ref;
+            res.inst = inst_ref;
+        }
+    } else {
+        shape_test<false>(sc, qs, ref, r, tmin, closest, inst_ref, res, cnt);
+    }
+}
 #ifndef GS_NESTED_WW
 #define GS_NESTED_WW 0  // 1: measured neutral on final_scene (2 142 vs 2 155, profiles/r04/ab_cube_records.txt)
 #endif
+template <bool SPH>
 __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs, uint32_t root, const Ray& r, double tmin,
                                            double closest, uint32_t inst_ref, LeafHit& res,
                                            unsigned long long* cnt) {
@@ -956,7 +983,7 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
             if (cur == THR_END) break;
         }
         if (cur == THR_END) break;
-        shape_test<false>(sc, qs, b.w, r, tmin, closest, inst_ref, res, cnt);
+        nested_leaf<SPH>(sc, qs, b.w, r, tmin, closest, inst_ref, res, cnt);
         if (res.hit) {  // res.t only ever shrinks
             closest = res.t;
             closest32 = (float)res.t;
@@ -977,7 +1004,7 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
             b = q[1];
         }
         if (b.z & NREC_LEAF) {  // a leaf occurrence: test it, then the next record
-            shape_test<false>(sc, qs, b.w, r, tmin, closest, inst_ref, res, cnt);
+            nested_leaf<SPH>(sc, qs, b.w, r, tmin, closest, inst_ref, res, cnt);
             if (res.hit) {  // res.t only ever shrinks
                 closest = res.t;
                 closest32 = (float)res.t;
@@ -1021,7 +1048,7 @@ __device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, const QuadSrc& qs,
     if ((FEAT & GS_FEAT_MEDIA) && (cur >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
         medium_test<UNI, (FEAT & GS_FEAT_NESTED) == 0>(sc, qs, cur, r, tmin, closest, inst_ref, rng, res, cnt);
     } else if ((FEAT & GS_FEAT_NESTED) && (cur >> GS_REF_SHIFT) == GS_REF_NODE) {
-        nested_bvh(sc, qs, cur & GS_REF_MASK, r, tmin, closest, inst_ref, res, cnt);
+        nested_bvh<(FEAT & GS_FEAT_NSPH) != 0>(sc, qs, cur & GS_REF_MASK, r, tmin, closest, inst_ref, res, cnt);
     } else {
         shape_test<UNI>(sc, qs, cur, r, tmin, closest, inst_ref, res, cnt);
     }
@@ -3415,7 +3442,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     // of the instances points its node children at their tree's first record.
     std::vector<DNode> nodes;
     std::vector<TNode> nrecs;  // nodes' f32 records (index-aligned)
-    bool nested_cert = true;
+    bool nested_cert = true, nested_sph = true;
     std::vector<gs_instance> insts(s->instances, s->instances + s->n_instances);
     {
         std::unordered_map<uint32_t, uint32_t> start;  // node index -> first record
@@ -3493,6 +3520,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         for (const DNode& n : nodes) {  // the f32 records (nested_bvh), index-aligned with nodes
             if (n.pad0) {
                 nrecs.push_back(TNode{0, 0, 0, 0, 0, 0, NREC_LEAF | n.left, n.right});
+                if ((n.right >> GS_REF_SHIFT) != GS_REF_SPHERE) nested_sph = false;
             } else {
                 nrecs.push_back(TNode{(float)n.mnx, (float)n.mny, (float)n.mxx, (float)n.mxy, (float)n.mnz, (float)n.mxz,
                                       n.left, n.right});
@@ -3802,6 +3830,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ds->other_leaf_frac = other_leaf_frac;
     ds->bvh_depth = depth < 1 ? 1 : depth;
     ds->feat = (s->n_media != 0 ? GS_FEAT_MEDIA : 0) | (nested ? GS_FEAT_NESTED : 0) | (leaf_runs ? GS_FEAT_LEAFRUN : 0);
+    if (nested && nested_sph && GS_NSPH) ds->feat |= GS_FEAT_NSPH;
     if (!(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED)) && lds_nodes == tnodes.size() && lds_leaves == tleaves.size())
         ds->feat |= GS_FEAT_LDSTREE;  // (cleared at launch if the device's LDS cannot hold it all)
     {  // staged shading when three or more of its sharing cases can meet in one wave
@@ -3911,6 +3940,13 @@ static void (*kernel_for(int feat))(KArgs) {
         case GS_FEAT_LEAFRUN | GS_FEAT_NESTED: return gs_render_kernel<GS_FEAT_LEAFRUN | GS_FEAT_NESTED>;
         case GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED:
             return gs_render_kernel<GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED>;
+        case GS_FEAT_NSPH | GS_FEAT_NESTED: return gs_render_kernel<GS_FEAT_NSPH | GS_FEAT_NESTED>;
+        case GS_FEAT_NSPH | GS_FEAT_MEDIA | GS_FEAT_NESTED:
+            return gs_render_kernel<GS_FEAT_NSPH | GS_FEAT_MEDIA | GS_FEAT_NESTED>;
+        case GS_FEAT_NSPH | GS_FEAT_LEAFRUN | GS_FEAT_NESTED:
+            return gs_render_kernel<GS_FEAT_NSPH | GS_FEAT_LEAFRUN | GS_FEAT_NESTED>;
+        case GS_FEAT_NSPH | GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED:
+            return gs_render_kernel<GS_FEAT_NSPH | GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED>;
         case GS_FEAT_LDSTREE: return gs_render_kernel<GS_FEAT_LDSTREE>;
         case GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN: return gs_render_kernel<GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN>;
         case GS_FEAT_MIXED: return gs_render_kernel<GS_FEAT_MIXED>;

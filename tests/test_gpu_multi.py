@@ -236,3 +236,33 @@ def test_concurrent_launches_of_one_scene():
         torch.cuda.synchronize()
         assert np.array_equal(frame.view(r.height, r.width, 3).cpu().numpy(), refs[s]), s
     r.close()
+
+
+def test_frame_context_from_two_threads():
+    """One frame context rendered from two host threads at once (gs_multi_render holds the
+    context's mutex, taken before anything reads its state): every frame equals the
+    one-shot render of its seed, the first frame's placement pilots run once."""
+    import threading
+    sc = scenes.config("C4", width=96, spp=4)
+    seeds = [1, 2, 3, 4, 5, 6]
+    refs = {s: g.render(sc, seed=s) for s in seeds}
+    m = g.MultiRenderer(sc, num_gpus=1, tile=32, plan=False)
+    got, errors = {}, []
+
+    def worker(k):
+        try:
+            for s in seeds[k::2]:
+                got[s] = m.render(seed=s, rgb=True)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errors, errors
+    for s in seeds:
+        assert np.array_equal(got[s]["rgb"], refs[s][0]) and got[s]["counters"] == refs[s][1], s
+    assert sum(1 for s in seeds if got[s]["stats"]["setup_ms"] > 0.0) <= 1
+    m.close()

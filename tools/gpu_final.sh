@@ -3,7 +3,8 @@
 # stamps"), each step under its own time limit, results under gpurun_out/$TAG:
 #   tests   the whole -m gpu suite
 #   bench   the default bench line (C4: parity + CPU baseline) and its rocprofv3 kernel stats
-#   pmc     tools/pmc.sh for every config named in PMC_CONFIGS (default C4 C3 C5 A2)
+#   pmc     tools/pmc.sh for every config named in PMC_CONFIGS (default C4 C3 C5 A2 final_scene;
+#           final_scene at 1440^2 x 64 spp)
 #   configs every BASELINE config at its stated size, with parity and the CPU baseline, plus
 #           the adaptive A1 / A2 and final_scene at 1440^2 x 64 spp
 #   stamps  the stamps build's phase split for C4, final_scene and cornell_smoke
@@ -26,8 +27,9 @@ bench)
   cat $O/stats_bench.json
   find $O/stats -name "*kernel_stats.csv" -exec head -6 {} \; ;;
 pmc)
-  for c in ${PMC_CONFIGS:-C4 C3 C5 A2}; do
-    CONFIG=$c bash $R/tools/pmc.sh || exit 1
+  for c in ${PMC_CONFIGS:-C4 C3 C5 A2 final_scene}; do
+    if [ $c = final_scene ]; then BA="--width 1440 --spp 64"; else BA=""; fi
+    CONFIG=$c BENCH_ARGS="$BA" bash $R/tools/pmc.sh || exit 1
   done ;;
 configs)
   for spec in "C1 1 3" "C2 4 1" "C3 8 1" "C4 3 3" "C5 24 1" "A1 3 1" "A2 8 1"; do
@@ -36,7 +38,9 @@ configs)
     python -c "import json; d=json.loads(open('$O/cfg_$1.json').read().strip().splitlines()[-1]); p=d['parity']; r=d['roofline']; print('$1', d['value'], 'Msamples/s', d['ms_per_step'], 'ms', 'parity max|d| %g over %d px' % (p['max_abs_delta'], p['pixels']), 'cpu', d['cpu_baseline']['value'], 'frac', r['frac'])"
   done
   timeout -k 10 300 python3 -u bench.py --config final_scene --width 1440 --spp 64 --steps 2 --warmup 1 --cpu-stride 4 --cpu-runs 1 > $O/final_scene_1440.json 2> $O/final_scene_1440.err || { echo "final_scene failed"; tail -5 $O/final_scene_1440.err; exit 1; }
-  python -c "import json; d=json.loads(open('$O/final_scene_1440.json').read().strip().splitlines()[-1]); print('final_scene', d['value'], d['ms_per_step'], d['parity']['max_abs_delta'], d['cpu_baseline']['value'])" ;;
+  python -c "import json; d=json.loads(open('$O/final_scene_1440.json').read().strip().splitlines()[-1]); print('final_scene', d['value'], d['ms_per_step'], d['parity']['max_abs_delta'], d['cpu_baseline']['value'], d['roofline']['frac'])"
+  timeout -k 10 300 python3 -u bench.py --config cornell_smoke --width 1440 --spp 64 --steps 2 --warmup 1 --cpu-stride 4 --cpu-runs 1 > $O/cornell_smoke_1440.json 2> $O/cornell_smoke_1440.err || { echo "cornell_smoke failed"; tail -5 $O/cornell_smoke_1440.err; exit 1; }
+  python -c "import json; d=json.loads(open('$O/cornell_smoke_1440.json').read().strip().splitlines()[-1]); print('cornell_smoke', d['value'], d['ms_per_step'], d['parity']['max_abs_delta'], d['cpu_baseline']['value'])" ;;
 stamps)
   for spec in "C4 1920 512" "final_scene 1440 64" "cornell_smoke 1440 64"; do
     set -- $spec
