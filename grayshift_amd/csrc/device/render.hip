@@ -143,6 +143,7 @@ struct DevScene {
     const DNode* nodes;   // nested trees' records with their f64 boxes (the f64 test)
     const TNode* nrecs;   // the same records for the certified f32 test (nested_bvh)
     uint32_t nested_cert; // every nested node coordinate |x| <= 1e15 (box_cert applies)
+    const double* nradii; // GS_FEAT_NSPH: the nested spheres' distinct radii (<= 16; nested_leaf)
     const DSphere* spheres;
     const uint32_t* sphere_mat;
     const gs_msphere* mspheres;
@@ -916,20 +917,24 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
 // dispatch; else the generic test.  (A runtime branch between the two, and |d|^2 hoisted
 // out of the walk, spilled 8-16 B/lane.)
 template <bool SPH>
-__device__ __forceinline__ void nested_leaf(const DevScene& sc, const QuadSrc& qs, uint32_t ref, const Ray& r, double tmin, double closest, uint32_t inst_ref, LeafHit& res,
+__device__ __forceinline__ void nested_leaf(const DevScene& sc, const QuadSrc& qs, const u32x4& a, const u32x4& b,
+                                            const Ray& r, double tmin, double closest, uint32_t inst_ref, LeafHit& res,
                                             unsigned long long* cnt) {
     if constexpr (SPH) {
+        // the sphere inline in the leaf record (set up with the nested records): its centre
+        // in the record's first 24 B, its index in the ref's index bits, its radius's slot
+        // in the scene's radius table in the ref's kind bits (the kind is a sphere here)
         atomicAdd(&cnt[C_SPH], 1ull);
-        const auto sp_ = sp<false>(sc.spheres + (ref & GS_REF_MASK));
+        const double rad = sp<false>(sc.nradii)[b.w >> GS_REF_SHIFT];
         double t;
-        if (sphere_accept(mk(sp_->cx, sp_->cy, sp_->cz), sp_->r, r, len2(r.d), tmin, closest, t)) {
+        if (sphere_accept(mk(lo_hi(a.x, a.y), lo_hi(a.z, a.w), lo_hi(b.x, b.y)), rad, r, len2(r.d), tmin, closest, t)) {
             res.hit = true;
             res.t = t;
-            res.ref = ref;
+            res.ref = GS_MAKE_REF(GS_REF_SPHERE, b.w & GS_REF_MASK);
             res.inst = inst_ref;
         }
     } else {
-        shape_test<false>(sc, qs, ref, r, tmin, closest, inst_ref, res, cnt);
+        shape_test<false>(sc, qs, b.w, r, tmin, closest, inst_ref, res, cnt);
     }
 }
 #ifndef GS_NESTED_WW
@@ -983,7 +988,7 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
             if (cur == THR_END) break;
         }
         if (cur == THR_END) break;
-        nested_leaf<SPH>(sc, qs, b.w, r, tmin, closest, inst_ref, res, cnt);
+        nested_leaf<SPH>(sc, qs, a, b, r, tmin, closest, inst_ref, res, cnt);
         if (res.hit) {  // res.t only ever shrinks
             closest = res.t;
             closest32 = (float)res.t;
@@ -1004,7 +1009,7 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
             b = q[1];
         }
         if (b.z & NREC_LEAF) {  // a leaf occurrence: test it, then the next record
-            nested_leaf<SPH>(sc, qs, b.w, r, tmin, closest, inst_ref, res, cnt);
+            nested_leaf<SPH>(sc, qs, a, b, r, tmin, closest, inst_ref, res, cnt);
             if (res.hit) {  // res.t only ever shrinks
                 closest = res.t;
                 closest32 = (float)res.t;
@@ -3443,6 +3448,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     std::vector<DNode> nodes;
     std::vector<TNode> nrecs;  // nodes' f32 records (index-aligned)
     bool nested_cert = true, nested_sph = true;
+    std::vector<double> nradii;  // the nested spheres' distinct radii (GS_FEAT_NSPH)
     std::vector<gs_instance> insts(s->instances, s->instances + s->n_instances);
     {
         std::unordered_map<uint32_t, uint32_t> start;  // node index -> first record
@@ -3517,10 +3523,35 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             for (gs_instance& in : insts)
                 if ((in.child >> GS_REF_SHIFT) == GS_REF_NODE) in.child = GS_MAKE_REF(GS_REF_NODE, npos[in.child & GS_REF_MASK]);
         }
+        // GS_FEAT_NSPH: every nested leaf a stationary sphere, of at most 16 distinct radii
+        for (const DNode& n : nodes) {
+            if (!n.pad0) continue;
+            if ((n.right >> GS_REF_SHIFT) != GS_REF_SPHERE || (n.right & GS_REF_MASK) >= s->n_spheres) {
+                nested_sph = false;
+                break;
+            }
+            const double rad = s->spheres[n.right & GS_REF_MASK].radius;
+            bool seen = false;
+            for (const double& x : nradii) seen |= std::memcmp(&x, &rad, 8) == 0;
+            if (!seen) nradii.push_back(rad);
+            if (nradii.size() > 16) {
+                nested_sph = false;
+                break;
+            }
+        }
+        if (!GS_NSPH || nodes.empty()) nested_sph = false;
+        if (!nested_sph) nradii.clear();
         for (const DNode& n : nodes) {  // the f32 records (nested_bvh), index-aligned with nodes
             if (n.pad0) {
-                nrecs.push_back(TNode{0, 0, 0, 0, 0, 0, NREC_LEAF | n.left, n.right});
-                if ((n.right >> GS_REF_SHIFT) != GS_REF_SPHERE) nested_sph = false;
+                TNode t{0, 0, 0, 0, 0, 0, NREC_LEAF | n.left, n.right};
+                if (nested_sph) {  // the sphere inline (nested_leaf)
+                    const gs_sphere& x = s->spheres[n.right & GS_REF_MASK];
+                    uint32_t slot = 0;
+                    while (std::memcmp(&nradii[slot], &x.radius, 8) != 0) slot++;
+                    std::memcpy(&t, x.center, 24);
+                    t.miss = (slot << GS_REF_SHIFT) | (n.right & GS_REF_MASK);
+                }
+                nrecs.push_back(t);
             } else {
                 nrecs.push_back(TNode{(float)n.mnx, (float)n.mny, (float)n.mxx, (float)n.mxy, (float)n.mnz, (float)n.mxz,
                                       n.left, n.right});
@@ -3740,6 +3771,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     Layout L;
     size_t o_nodes = L.add(nodes.data(), nodes.size() * sizeof(DNode));
     size_t o_nrecs = L.add(nrecs.data(), nrecs.size() * sizeof(TNode));
+    size_t o_nradii = L.add(nradii.data(), nradii.size() * sizeof(double));
     size_t o_tnodes = L.add(tnodes.data(), tnodes.size() * sizeof(TNode));
     size_t o_tboxes = L.add(tboxes.data(), tboxes.size() * sizeof(TBox));
     size_t o_tleaves = L.add(tleaves.data(), tleaves.size() * sizeof(TLeaf));
@@ -3782,6 +3814,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     d.nodes = (const DNode*)(b + o_nodes);
     d.nrecs = (const TNode*)(b + o_nrecs);
     d.nested_cert = nested_cert ? 1u : 0u;
+    d.nradii = (const double*)(b + o_nradii);
     d.spheres = (const DSphere*)(b + o_sph);
     d.sphere_mat = (const uint32_t*)(b + o_sphm);
     d.mspheres = (const gs_msphere*)(b + o_msph);
@@ -3830,7 +3863,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ds->other_leaf_frac = other_leaf_frac;
     ds->bvh_depth = depth < 1 ? 1 : depth;
     ds->feat = (s->n_media != 0 ? GS_FEAT_MEDIA : 0) | (nested ? GS_FEAT_NESTED : 0) | (leaf_runs ? GS_FEAT_LEAFRUN : 0);
-    if (nested && nested_sph && GS_NSPH) ds->feat |= GS_FEAT_NSPH;
+    if (nested && nested_sph) ds->feat |= GS_FEAT_NSPH;
     if (!(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED)) && lds_nodes == tnodes.size() && lds_leaves == tleaves.size())
         ds->feat |= GS_FEAT_LDSTREE;  // (cleared at launch if the device's LDS cannot hold it all)
     {  // staged shading when three or more of its sharing cases can meet in one wave
@@ -3955,6 +3988,7 @@ static void (*kernel_for(int feat))(KArgs) {
         case GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN:
             return gs_render_kernel<GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN>;
         case GS_FEAT_PILOT: return gs_render_kernel<GS_FEAT_PILOT>;
+        case GS_FEAT_PILOT | GS_FEAT_NSPH: return gs_render_kernel<GS_FEAT_PILOT | GS_FEAT_NSPH>;  // (the inline nested spheres' format)
         case GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN: return gs_render_kernel<GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN>;
         case GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_LDSTREE:
             return gs_render_kernel<GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_LDSTREE>;
@@ -4309,7 +4343,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
 #else
     const bool pilot_kernel = va != nullptr || (GS_SALU_COUNT && outs->item_visits != nullptr);
 #endif
-    hipLaunchKernelGGL(kernel_for(pilot_kernel ? GS_FEAT_PILOT : lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
+    hipLaunchKernelGGL(kernel_for(pilot_kernel ? (GS_FEAT_PILOT | (lc.feat & GS_FEAT_NSPH)) : lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
     if (k_end) HIPCHK(hipEventRecord(k_end, st));
     if (chunk) {
