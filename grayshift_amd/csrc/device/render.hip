@@ -916,6 +916,9 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
 // box of balls, main.rs:741-755; GS_FEAT_NSPH), Sphere::hit directly, with no kind
 // dispatch; else the generic test.  (A runtime branch between the two, and |d|^2 hoisted
 // out of the walk, spilled 8-16 B/lane.)
+#ifndef GS_NRAD_UNIFORM
+#define GS_NRAD_UNIFORM 1
+#endif
 template <bool SPH>
 __device__ __forceinline__ void nested_leaf(const DevScene& sc, const QuadSrc& qs, const u32x4& a, const u32x4& b,
                                             const Ray& r, double tmin, double closest, uint32_t inst_ref, LeafHit& res,
@@ -925,7 +928,14 @@ __device__ __forceinline__ void nested_leaf(const DevScene& sc, const QuadSrc& q
         // in the record's first 24 B, its index in the ref's index bits, its radius's slot
         // in the scene's radius table in the ref's kind bits (the kind is a sphere here)
         atomicAdd(&cnt[C_SPH], 1ull);
+#if GS_NRAD_UNIFORM
+        // (a wave whose lanes share the radius slot -- one radius in the scene: always --
+        // reads it with a scalar load)
+        const uint32_t slot = b.w >> GS_REF_SHIFT, s0 = __builtin_amdgcn_readfirstlane(slot);
+        const double rad = __builtin_amdgcn_ballot_w64(slot != s0) == 0 ? sp<true>(sc.nradii)[s0] : sp<false>(sc.nradii)[slot];
+#else
         const double rad = sp<false>(sc.nradii)[b.w >> GS_REF_SHIFT];
+#endif
         double t;
         if (sphere_accept(mk(lo_hi(a.x, a.y), lo_hi(a.z, a.w), lo_hi(b.x, b.y)), rad, r, len2(r.d), tmin, closest, t)) {
             res.hit = true;
