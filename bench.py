@@ -141,7 +141,7 @@ def main():
 def load_scene(a):
     import grayshift_amd as g
     from grayshift_amd import scenes
-    g.set_tuning(a.shade_batch or 52, a.blocks_per_cu or 0, 0 if a.leaf_batch is None else a.leaf_batch,
+    g.set_tuning(a.shade_batch or 0, a.blocks_per_cu or 0, 0 if a.leaf_batch is None else a.leaf_batch,
                  -1 if a.sample_chunk is None else a.sample_chunk)
     g._native.check(g._native.lib.gs_set_node_steps(a.node_steps))
     g._native.check(g._native.lib.gs_set_adaptive_mode(a.adaptive_mode))

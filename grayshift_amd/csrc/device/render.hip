@@ -2827,12 +2827,15 @@ __global__ void gs_round_combine_kernel(const KParams* __restrict__ P, uint32_t 
 
 // =============================================================== host side
 static thread_local std::string tl_err;
-static int32_t g_shade_batch = 52;  // swept on MI355X C4 (chunked, uniform loop): 48 -> 3502, 52 -> 3535-3568, 56 -> 3506-3536 Msamples/s
+static int32_t g_shade_batch = 0;   // 0: the scene's own (52, or GS_KIND_SHADE_BATCH with BVHs under instances);  // swept on MI355X C4 (chunked, uniform loop): 48 -> 3502, 52 -> 3535-3568, 56 -> 3506-3536 Msamples/s
 static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
 static int32_t g_node_steps = 0;  // 0: the scene's own (gs_device_scene.node_steps)
 // leaf batch: 0 = the scene's choice (12: swept on MI355X C4 with leaf runs: 8 -> 4586, 10 ->
 // 4632, 12 -> 4648-4651, 14 -> 4624, 16 -> 4592; GS_KIND_LEAF_BATCH for kind-batched kernels)
 static int32_t g_leaf_batch = 0;
+#ifndef GS_KIND_SHADE_BATCH
+#define GS_KIND_SHADE_BATCH 44
+#endif
 #ifndef GS_KIND_LEAF_BATCH
 #define GS_KIND_LEAF_BATCH 48
 #endif
@@ -2937,6 +2940,7 @@ struct gs_device_scene {
     const TNode* nrecs = nullptr;
     int32_t node_steps = GS_NODE_STEPS;      // node steps per node pass (from the tree's shape)
     int32_t leaf_batch = 12;                 // lanes at a leaf before a leaf pass (scene's choice)
+    int32_t shade_batch = 52;                // finished lanes a wave shades together (scene's choice)
     uint32_t node_records = 0, leaf_records = 0;
     double nodes_per_leaf = 0.0, other_leaf_frac = 0.0;
     // Launch state, mutated by launches of a const scene: guarded by `mu`.
@@ -3380,7 +3384,7 @@ gs_status gs_set_node_steps(int32_t node_steps) {
 }
 
 gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf_batch, int32_t sample_chunk) {
-    if (shade_batch < 1 || shade_batch > 64 || blocks_per_cu < 0 || blocks_per_cu > 8 || leaf_batch < 0 ||
+    if (shade_batch < 0 || shade_batch > 64 || blocks_per_cu < 0 || blocks_per_cu > 8 || leaf_batch < 0 ||
         leaf_batch > 64 || sample_chunk < -1)
         return fail(GS_ERR_ARG, "bad tuning");
     g_sample_chunk = sample_chunk;
@@ -3895,8 +3899,12 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     // final_scene 1440^2 x 64 spp, (leaf batch, node steps): (12, 1) 1206, (32, 3) 1540,
     // (48, 3) 1594, (48, 8) 1679, (64, 8) 1662 Msamples/s (profiles/r03/sweep_final_scene_
     // leaf_batch*.txt).  Not for staged shading alone: C5 leaf batch 12 6178, 24 5989, 48 5236.
+    // ... and shade smaller batches (round 4, after the nested-leaf changes; shade batch x leaf
+    // batch at 8 node steps, twice: 44 / 48: 2 396, 2 462; 44 / 56: 2 449, 2 453; 52 / 48:
+    // 2 365, 2 398 Msamples/s, profiles/r04/sweep_final_scene_shade_leaf_batch.txt).
     if (ds->feat & GS_FEAT_NESTED) {
         ds->leaf_batch = GS_KIND_LEAF_BATCH;
+        ds->shade_batch = GS_KIND_SHADE_BATCH;
         ds->node_steps = std::max<int32_t>(ds->node_steps, GS_KIND_NODE_STEPS);
     }
     ds->tree = std::move(tree_keep);
@@ -4179,7 +4187,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     a.tquads = ds->tquads;
     a.root = ds->thr_root;
     a.cert_boxes = ds->cert_boxes ? 1 : 0;
-    a.shade_batch = g_shade_batch;
+    a.shade_batch = g_shade_batch > 0 ? g_shade_batch : ds->shade_batch;
     a.leaf_batch = std::max<int32_t>(1, g_leaf_batch > 0 ? g_leaf_batch : ds->leaf_batch);  // (0 would never step a node)
     a.node_steps = std::max(1, std::min<int32_t>(GS_NODE_STEPS, g_node_steps > 0 ? g_node_steps : ds->node_steps));
     gs_device_scene* mds = const_cast<gs_device_scene*>(ds);

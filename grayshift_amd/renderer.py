@@ -179,7 +179,7 @@ def ppm_encode_async(d_rgb8, width, height, d_text, text_capacity, d_len, d_scra
                                       C.c_void_p(d_len), C.c_void_p(d_scratch), scratch_bytes, C.c_void_p(stream)))
 
 
-def set_tuning(shade_batch=52, blocks_per_cu=0, leaf_batch=0, sample_chunk=-1):
+def set_tuning(shade_batch=0, blocks_per_cu=0, leaf_batch=0, sample_chunk=-1):
     """Process-wide launch tuning (see gs_set_tuning in include/grayshift_gpu.h)."""
     N.check(N.lib.gs_set_tuning(shade_batch, blocks_per_cu, leaf_batch, sample_chunk))
 

@@ -212,8 +212,9 @@ typedef struct gs_device_scene gs_device_scene;
 const char* gs_last_error(void);
 int32_t gs_version(void);
 
-/* Launch tuning, process-wide: shade_batch in [1, 64] = finished lanes a wave
- * collects before it shades them together; blocks_per_cu in [0, 8], 0 = from the
+/* Launch tuning, process-wide: shade_batch in [0, 64] = finished lanes a wave
+ * collects before it shades them together (0 = the scene's own choice: 52, or 44 for
+ * scenes with BVHs under instances; ABI 8); blocks_per_cu in [0, 8], 0 = from the
  * occupancy query; leaf_batch in [0, 64] = lanes waiting at a leaf before the wave
  * runs a leaf-test pass (0 = the scene's own choice: 12, or 48 for scenes with BVHs
  * under instances, whose leaf passes serve one leaf kind each);

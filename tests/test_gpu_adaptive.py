@@ -36,7 +36,7 @@ class _mode:
 
     def __exit__(self, *a):
         N.check(N.lib.gs_set_adaptive_mode(1))
-        g.set_tuning(52, 0, 0, -1)
+        g.set_tuning(0, 0, 0, -1)
         N.check(N.lib.gs_debug_set_partial_budget(0))
         N.check(N.lib.gs_debug_set_round_items(0))
 

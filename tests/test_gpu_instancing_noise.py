@@ -101,7 +101,7 @@ def test_final_scene_is_independent_of_leaf_batch_and_node_steps():
             N.check(N.lib.gs_set_node_steps(ns))
             runs.append(g.render(sc, seed=5))
     finally:
-        g.set_tuning(52, 0, 0, -1)
+        g.set_tuning(0, 0, 0, -1)
         N.check(N.lib.gs_set_node_steps(0))
     for out, gc in runs:
         assert np.array_equal(out, runs[0][0]) and gc == runs[0][1]

@@ -228,7 +228,7 @@ class _chunk:
         g.set_tuning(52, 0, 0, self.n)
 
     def __exit__(self, *a):
-        g.set_tuning(52, 0, 0, -1)
+        g.set_tuning(0, 0, 0, -1)
 
 
 @pytest.mark.parametrize("name", ["C4", "C3", "earth_fixed"])

@@ -40,11 +40,13 @@ def test_every_declared_symbol_is_exported(built):
 
 def test_version_and_error_channel():
     assert N.lib.gs_version() == N.GS_ABI_VERSION == 8
-    assert N.lib.gs_set_tuning(0, 0, 0, -1) == N.GS_ERR_ARG
+    assert N.lib.gs_set_tuning(-1, 0, 0, -1) == N.GS_ERR_ARG
     assert b"tuning" in N.lib.gs_last_error()
+    assert N.lib.gs_set_tuning(65, 0, 0, -1) == N.GS_ERR_ARG
     assert N.lib.gs_set_tuning(60, 0, 0, -1) == N.GS_OK
     assert N.lib.gs_set_tuning(60, 0, 8, -2) == N.GS_ERR_ARG
     assert N.lib.gs_set_tuning(60, 0, 8, -1) == N.GS_OK
+    assert N.lib.gs_set_tuning(0, 0, 0, -1) == N.GS_OK  # (0: the scene's own shade batch, ABI 8)
 
 
 @pytest.mark.parametrize("name", ["gs_object", "gs_material_spec", "gs_texture_spec", "gs_image_spec",

@@ -36,7 +36,7 @@ def main():
                                for t in [int(x) for x in a.tiles.split(",")]
                                for c in [int(x) for x in a.chunks.split(",")]]:
         if True:
-            g.set_tuning(52, 0, 0, chunk)
+            g.set_tuning(0, 0, 0, chunk)
             for rank in [int(x) for x in a.ranks.split(",")]:
                 if rank >= world:
                     continue

@@ -11,7 +11,7 @@ def main():
     ap.add_argument("--config", default="C4")
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
-    ap.add_argument("--shade-batch", type=int, default=52)
+    ap.add_argument("--shade-batch", type=int, default=0, help="0: the scene's own")
     ap.add_argument("--leaf-batch", type=int, default=0, help="0: the scene's choice")
     ap.add_argument("--sample-chunk", type=int, default=-1)
     ap.add_argument("--node-steps", type=int, default=0, help="0: the scene's own")
