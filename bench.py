@@ -414,9 +414,15 @@ def roofline(a, c, world, kernel_ms, invalid):
     clock = k["GRBM_GUI_ACTIVE"] / 8.0 / prof_s  # effective shader clock of the profiled launch (Hz)
     cyc, mix = valu_cycles(k)
     cyc_hi, _ = valu_cycles(k, VALU_CYCLES_UPPER)
+    n_disp0 = int(pj.get("dispatches_per_frame", 1) or 1)
+    cyc1 = cyc
+    cyc, cyc_hi = cyc * n_disp0, cyc_hi * n_disp0
     busy = None
     if "SQ_ACTIVE_INST_VALU2" in k and "SQ_ACTIVE_INST_VALU" in k:
         busy = 4.0 * (float(k["SQ_ACTIVE_INST_VALU"]) - float(k["SQ_ACTIVE_INST_VALU2"]))
+    # the counters are per megakernel launch; a frame of batch rounds launches it once per
+    # round (and segment): the frame's VALU work is that many launches' over the frame's time
+    busy = None if busy is None else busy * n_disp0
     peak = SIMDS * clock
     achieved = (busy if busy is not None else cyc) / kernel_s  # VALU issue cycles per second, all SIMDs
     wc = float(k.get("SQ_WAVE_CYCLES", 0.0)) or 1.0
@@ -427,8 +433,9 @@ def roofline(a, c, world, kernel_ms, invalid):
                 "traffic": pj["hbm_bytes_per_launch"],
                 "hbm_frac": round(pj["hbm_bytes_per_launch"] / kernel_s / 1e9 / HBM_PEAK_GBS, 5),
                 "effective_clock_ghz": round(clock / 1e9, 3),
-                "valu_instructions": int(k["SQ_INSTS_VALU"]),
-                "valu_cycle_mix": {c2: round(v[1] / cyc, 4) for c2, v in mix.items()},
+                "valu_instructions": int(k["SQ_INSTS_VALU"]) * n_disp0,
+                "launches_per_frame": n_disp0,
+                "valu_cycle_mix": {c2: round(v[1] / cyc1, 4) for c2, v in mix.items()},
                 "wave_cycles_waiting": round(float(k.get("SQ_WAIT_ANY", 0.0)) / wc, 4),
                 "wave_cycles_issue_stalled": round(float(k.get("SQ_WAIT_INST_ANY", 0.0)) / wc, 4),
                 "wave_cycles_issuing": round(float(k.get("SQ_ACTIVE_INST_ANY", 0.0)) / wc, 4),

@@ -59,6 +59,9 @@ def main():
         "source": "tools/pmc.sh on MI355X: rocprofv3 --kernel-trace --pmc, one pass per counter group, "
                   "one frame per pass; folded by tools/pmc_summary.py",
         "kernel_duration_ms_profiled": sum(dur) / len(dur) if dur else None,
+        # megakernel launches in one frame (one per batch round and sample-buffer segment for
+        # adaptive settings; 1 otherwise): the counters above are per launch
+        "dispatches_per_frame": len(dispatches.get("SQ_ACTIVE_INST_VALU", dispatches[next(iter(dispatches))])),
         "counters": c,
         "fetch_bytes_raw": fetch, "write_bytes_raw": write,
         "hbm_bytes_per_launch": 2 * fetch + write,
@@ -76,6 +79,8 @@ def main():
         out["valu_issue_frac"] = c["SQ_INSTS_VALU"] * 4 / (1024 * cyc)
         if "SQ_ACTIVE_INST_VALU" in c:
             out["valu_active_frac"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * cyc)
+            if "SQ_ACTIVE_INST_VALU2" in c:  # the measured busy fraction bench.py reports
+                out["valu_busy_frac"] = 4 * (c["SQ_ACTIVE_INST_VALU"] - c["SQ_ACTIVE_INST_VALU2"]) / (1024 * cyc)
         if "SQ_INSTS_SALU" in c:
             out["salu_issue_frac"] = c["SQ_INSTS_SALU"] / (1024 * cyc)
     if "SQ_LDS_IDX_ACTIVE" in c and "GRBM_GUI_ACTIVE" in c:
