@@ -402,9 +402,12 @@ def roofline(a, c, world, kernel_ms, invalid):
         out["pmc"] = "no code-object hash: %s" % e
         return out
     out["code_object"] = h
-    if invalid or world != 1:
-        return out  # the PMC summaries are 1-GPU whole-frame figures of the metric's config
-    path = os.path.join(a.pmc_dir, "%s_%s.json" % (a.config, h))
+    if world != 1:
+        return out  # the PMC summaries are 1-GPU whole-frame figures of one config
+    # (an overridden size has its own summary: <config>_w<width>_s<spp>_<hash>.json, e.g.
+    # final_scene at 1440^2 x 64 spp from tools/gpu_final.sh)
+    key = a.config if not invalid else "%s_w%s_s%s" % (a.config, a.width, a.spp)
+    path = os.path.join(a.pmc_dir, "%s_%s.json" % (key, h))
     if not os.path.exists(path):
         out["pmc"] = "none for this code object (%s)" % os.path.relpath(path, ROOT)
         return out

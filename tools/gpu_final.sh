@@ -28,8 +28,8 @@ bench)
   find $O/stats -name "*kernel_stats.csv" -exec head -6 {} \; ;;
 pmc)
   for c in ${PMC_CONFIGS:-C4 C3 C5 A2 final_scene}; do
-    if [ $c = final_scene ]; then BA="--width 1440 --spp 64"; else BA=""; fi
-    CONFIG=$c BENCH_ARGS="$BA" bash $R/tools/pmc.sh || exit 1
+    if [ $c = final_scene ]; then BA="--width 1440 --spp 64"; PT=final_scene_w1440_s64; else BA=""; PT=$c; fi
+    CONFIG=$c BENCH_ARGS="$BA" PMC_TAG=$PT bash $R/tools/pmc.sh || exit 1
   done ;;
 configs)
   for spec in "C1 1 3" "C2 4 1" "C3 8 1" "C4 3 3" "C5 24 1" "A1 3 1" "A2 8 1"; do

@@ -18,4 +18,5 @@ for set in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $set --output-format csv -d $O/pmc_$i -o run -- python3 $R/bench.py $ARGS > $O/pmc_$i.log 2>&1 || { echo "pass $i ($set) failed"; tail -3 $O/pmc_$i.log; exit 1; }
   echo "pass $i ok: $set"
 done
-python3 $R/tools/pmc_summary.py $O $R/gpurun_out/pmc_out --config $CONFIG --round 4
+# (PMC_TAG: the summary's name for an overridden size, e.g. final_scene_w1440_s64, bench.py)
+python3 $R/tools/pmc_summary.py $O $R/gpurun_out/pmc_out --config ${PMC_TAG:-$CONFIG} --round 4
