@@ -919,15 +919,19 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
 #ifndef GS_NRAD_UNIFORM
 #define GS_NRAD_UNIFORM 1
 #endif
-template <bool SPH>
+#ifndef GS_NESTED_LANE_COUNT
+#define GS_NESTED_LANE_COUNT 1
+#endif
+template <bool SPH, bool LC>
 __device__ __forceinline__ void nested_leaf(const DevScene& sc, const QuadSrc& qs, const u32x4& a, const u32x4& b,
                                             const Ray& r, double tmin, double closest, uint32_t inst_ref, LeafHit& res,
-                                            unsigned long long* cnt) {
+                                            unsigned long long* cnt, uint32_t& n_sph) {
     if constexpr (SPH) {
         // the sphere inline in the leaf record (set up with the nested records): its centre
         // in the record's first 24 B, its index in the ref's index bits, its radius's slot
         // in the scene's radius table in the ref's kind bits (the kind is a sphere here)
-        atomicAdd(&cnt[C_SPH], 1ull);
+        if constexpr (LC) n_sph++;
+        else atomicAdd(&cnt[C_SPH], 1ull);
 #if GS_NRAD_UNIFORM
         // (a wave whose lanes share the radius slot -- one radius in the scene: always --
         // reads it with a scalar load)
@@ -950,7 +954,7 @@ __device__ __forceinline__ void nested_leaf(const DevScene& sc, const QuadSrc& q
 #ifndef GS_NESTED_WW
 #define GS_NESTED_WW 0  // 1: measured neutral on final_scene (2 142 vs 2 155, profiles/r04/ab_cube_records.txt)
 #endif
-template <bool SPH>
+template <bool SPH, bool LC>
 __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs, uint32_t root, const Ray& r, double tmin,
                                            double closest, uint32_t inst_ref, LeafHit& res,
                                            unsigned long long* cnt) {
@@ -964,6 +968,14 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
     }
     float closest32 = (float)closest;
     uint32_t cur = root;
+    // (LC: the walk's node visits and sphere tests counted in registers and added to the
+    // block's counters once per walk -- per visit, the LDS atomic and its wave reduction
+    // cost ~4 SALU and 3 VALU.  Not in the media + sphere-run kernels, which spill with it.)
+    uint32_t n_nodes = 0, n_sph = 0;
+    auto count_node = [&]() __attribute__((always_inline)) {
+        if constexpr (LC) n_nodes++;
+        else atomicAdd(&cnt[C_NODES], 1ull);
+    };
 #if GS_NESTED_WW
     // "while-while": node steps until every lane of the walk sits at a leaf or has ended,
     // then the leaf lanes test their leaves together (a sphere test costs several node
@@ -984,7 +996,7 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
                 b = q[1];
             }
             if (b.z & NREC_LEAF) break;
-            atomicAdd(&cnt[C_NODES], 1ull);
+            count_node();
             bool h = false, undecided = true;
             if (fast)
                 h = box_cert(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(b.x), __uint_as_float(a.z),
@@ -998,7 +1010,7 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
             if (cur == THR_END) break;
         }
         if (cur == THR_END) break;
-        nested_leaf<SPH>(sc, qs, a, b, r, tmin, closest, inst_ref, res, cnt);
+        nested_leaf<SPH, LC>(sc, qs, a, b, r, tmin, closest, inst_ref, res, cnt, n_sph);
         if (res.hit) {  // res.t only ever shrinks
             closest = res.t;
             closest32 = (float)res.t;
@@ -1019,14 +1031,14 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
             b = q[1];
         }
         if (b.z & NREC_LEAF) {  // a leaf occurrence: test it, then the next record
-            nested_leaf<SPH>(sc, qs, a, b, r, tmin, closest, inst_ref, res, cnt);
+            nested_leaf<SPH, LC>(sc, qs, a, b, r, tmin, closest, inst_ref, res, cnt, n_sph);
             if (res.hit) {  // res.t only ever shrinks
                 closest = res.t;
                 closest32 = (float)res.t;
             }
             cur = b.z & ~NREC_LEAF;
         } else {
-            atomicAdd(&cnt[C_NODES], 1ull);
+            count_node();
             bool h = false, undecided = true;
             if (fast)
                 h = box_cert(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(b.x), __uint_as_float(a.z),
@@ -1042,6 +1054,12 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
         }
     }
 #endif
+    if constexpr (LC) {
+        atomicAdd(&cnt[C_NODES], (unsigned long long)n_nodes);
+        if constexpr (SPH) atomicAdd(&cnt[C_SPH], (unsigned long long)n_sph);
+    }
+    (void)n_sph;
+    (void)n_nodes;
 }
 
 // The rarer non-node children (everything but a stationary sphere reached directly
@@ -1063,7 +1081,9 @@ __device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, const QuadSrc& qs,
     if ((FEAT & GS_FEAT_MEDIA) && (cur >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
         medium_test<UNI, (FEAT & GS_FEAT_NESTED) == 0>(sc, qs, cur, r, tmin, closest, inst_ref, rng, res, cnt);
     } else if ((FEAT & GS_FEAT_NESTED) && (cur >> GS_REF_SHIFT) == GS_REF_NODE) {
-        nested_bvh<(FEAT & GS_FEAT_NSPH) != 0>(sc, qs, cur & GS_REF_MASK, r, tmin, closest, inst_ref, res, cnt);
+        nested_bvh<(FEAT & GS_FEAT_NSPH) != 0,
+                   GS_NESTED_LANE_COUNT && (FEAT & (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)) != (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)>(
+            sc, qs, cur & GS_REF_MASK, r, tmin, closest, inst_ref, res, cnt);
     } else {
         shape_test<UNI>(sc, qs, cur, r, tmin, closest, inst_ref, res, cnt);
     }
