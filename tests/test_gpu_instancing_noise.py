@@ -31,9 +31,10 @@ def test_scene_matches_oracle(name, width, spp):
         assert gc["instance_tests"] > 0 and gc["medium_tests"] > 0
 
 
-def nested_scene(width=40, spp=8, depth_chain=2, leaf="spheres"):
+def nested_scene(width=40, spp=8, depth_chain=2, leaf="spheres", radii=1):
     """A BVH of spheres / cubes (lists) / triangles under a Translate/RotateY chain,
-    next to top-level geometry."""
+    next to top-level geometry.  `radii`: distinct sphere radii (all-sphere trees of at most
+    16 take the inline nested-sphere records, GS_FEAT_NSPH; more take the generic test)."""
     b = g.SceneBuilder()
     rng = np.random.default_rng(7)
     white = b.lambertian((0.73, 0.73, 0.73))
@@ -44,7 +45,7 @@ def nested_scene(width=40, spp=8, depth_chain=2, leaf="spheres"):
         c = tuple(float(v) for v in rng.uniform(-3, 3, 3))
         m = (white, metal, glass)[k % 3]
         if leaf == "spheres" or k % 3 == 0:
-            members.append(b.sphere(c, 0.3, m))
+            members.append(b.sphere(c, 0.3 + 0.01 * (k % radii), m))
         elif leaf == "cubes":
             members.append(b.cube(c, (c[0] + 0.4, c[1] + 0.5, c[2] + 0.3), m))
         else:
@@ -63,10 +64,15 @@ def nested_scene(width=40, spp=8, depth_chain=2, leaf="spheres"):
     return scenes.Scene("nested", b.build(), cam, fixed_spp(spp))
 
 
-@pytest.mark.parametrize("leaf", ["spheres", "cubes", "triangles"])
+@pytest.mark.parametrize("leaf,radii", [("spheres", 1), ("spheres", 16), ("spheres", 17), ("cubes", 1),
+                                        ("triangles", 1)])
 @pytest.mark.parametrize("depth_chain", [1, 3])
-def test_nested_bvh_variants_match_oracle(leaf, depth_chain):
-    sc = nested_scene(leaf=leaf, depth_chain=depth_chain)
+def test_nested_bvh_variants_match_oracle(leaf, radii, depth_chain):
+    sc = nested_scene(leaf=leaf, depth_chain=depth_chain, radii=radii)
+    r = g.Renderer(sc)
+    nsph = (r.scene_info()["feat"] & 128) != 0  # GS_FEAT_NSPH: the inline nested-sphere records
+    r.close()
+    assert nsph == (leaf == "spheres" and radii <= 16)
     out, gc = g.render(sc, seed=4)
     ref, rc = oracle.render(sc, seed=4)
     assert maxdiff(out, ref) < TOL
