@@ -706,6 +706,9 @@ __device__ __forceinline__ void chain_count(const DevScene& sc, uint32_t cur, un
 #ifndef GS_CUBE_LDS
 #define GS_CUBE_LDS 1  // mirror a prefix of the cube records in LDS (after the other mirrors)
 #endif
+#ifndef GS_CUBE_ORDER
+#define GS_CUBE_ORDER 0  // 1: largest boxes first; measured neutral on final_scene (profiles/r04/ab_cube_order.txt)
+#endif
 #define GS_CUBE_FLAG 0x80000000u
 #define GS_CUBE_DOUBLES 12
 __host__ __device__ constexpr int cube_code(int k) { return k == 0 || k == 2 ? 4 : (k == 1 || k == 3 ? 1 : 3); }
@@ -3461,13 +3464,30 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     std::vector<gs_list> dlists(s->lists, s->lists + s->n_lists);
     std::vector<double> cubes;
     std::vector<uint8_t> in_cube(s->n_quads, 0);
-    for (uint32_t i = 0; GS_CUBE && g_cube_lists && i < s->n_lists; i++) {
-        double rec[GS_CUBE_DOUBLES];
-        uint32_t q0;
-        if (!cube_record(*s, s->lists[i], q0, rec)) continue;
-        dlists[i] = gs_list{(uint32_t)(cubes.size() / GS_CUBE_DOUBLES), GS_CUBE_FLAG | q0};
-        cubes.insert(cubes.end(), rec, rec + GS_CUBE_DOUBLES);
-        for (uint32_t k = 0; k < 6; k++) in_cube[q0 + k] = 1;
+    {
+        struct Cube {
+            uint32_t list, q0;
+            double area;
+            double rec[GS_CUBE_DOUBLES];
+        };
+        std::vector<Cube> found;
+        for (uint32_t i = 0; GS_CUBE && g_cube_lists && i < s->n_lists; i++) {
+            Cube c;
+            if (!cube_record(*s, s->lists[i], c.q0, c.rec)) continue;
+            c.list = i;
+            const double dx = c.rec[6], dy = c.rec[7], dz = c.rec[8];
+            c.area = std::fabs(dx * dy) + std::fabs(dy * dz) + std::fabs(dx * dz);
+            found.push_back(c);
+        }
+        // The LDS mirror holds a prefix of the cube records: the largest boxes first (the
+        // ones rays meet most, by surface area; GS_CUBE_ORDER 0 keeps list order).
+        if (GS_CUBE_ORDER)
+            std::stable_sort(found.begin(), found.end(), [](const Cube& x, const Cube& y) { return x.area > y.area; });
+        for (const Cube& c : found) {
+            dlists[c.list] = gs_list{(uint32_t)(cubes.size() / GS_CUBE_DOUBLES), GS_CUBE_FLAG | c.q0};
+            cubes.insert(cubes.end(), c.rec, c.rec + GS_CUBE_DOUBLES);
+            for (uint32_t k = 0; k < 6; k++) in_cube[c.q0 + k] = 1;
+        }
     }
     // (a quad may also be referenced directly elsewhere: any ref outside a cube list keeps
     // it a mirror candidate -- conservatively, every quad not in a cube list)
