@@ -37,7 +37,7 @@ def test_product_kernels_have_no_scratch(built):
     launch per scene; 183 with the nested sphere-leaf format) are the exception, and stay small."""
     scratch = codeobj.kernel_scratch(LIB_PATH)
     render = {k: v for k, v in scratch.items() if "gs_render_kernel" in k}
-    assert len(render) >= 19
+    assert len(render) >= 24  # 22 product instantiations + the two pilots
     for pilot in ("_Z16gs_render_kernelILi55EEv5KArgs", "_Z16gs_render_kernelILi183EEv5KArgs"):  # (+ GS_FEAT_NSPH)
         assert scratch.pop(pilot) <= 64
     assert {k: v for k, v in scratch.items() if v} == {}
