@@ -97,6 +97,19 @@ using namespace gsd;
 #endif
 #define GS_FEAT_NSPH 128   // with GS_FEAT_NESTED: every nested leaf is a stationary sphere
                            // (nested_leaf without the kind dispatch)
+#ifndef GS_NODE_STEPS
+#define GS_NODE_STEPS 8  // node steps per unrolled node pass (the render kernel, below)
+#endif
+// Kernels for scenes with nested sphere trees (GS_FEAT_NSPH: final_scene) may unroll a
+// different count (their node passes carry few lanes, 16.7 of 64): 16 measured final_scene
+// 2 469-2 521 against 8's 2 439-2 528 over four runs each -- within the spread, so 8; C4 with
+// 16 unrolled for every kernel: -0.4%, with 12: -1.3% (profiles/r04/ab_node_steps_unroll.txt).
+#ifndef GS_NSPH_NODE_STEPS
+#define GS_NSPH_NODE_STEPS 8  // 16: neutral within run-to-run spread (mean of four runs +1.2%)
+#endif
+__host__ __device__ constexpr int unroll_steps(int feat) {
+    return (feat & GS_FEAT_NSPH) != 0 ? GS_NSPH_NODE_STEPS : GS_NODE_STEPS;
+}
 // The pilot's instantiation: every code path (any scene), plus the counts.
 #define GS_FEAT_PILOT (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_VISITS)
 
@@ -1664,6 +1677,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #endif
     // BVHs under instances keep round 1's advance / begin_ray sites (see the shade pass)
     constexpr bool kOldSites = GS_NESTED_SITES && (FEAT & GS_FEAT_NESTED) != 0;
+    constexpr int kUnroll = unroll_steps(FEAT);  // node steps of an unrolled node pass
     // Every top-level leaf a stationary sphere: no instance is ever hit, so the hit's
     // instance (lane state L_HINST) stays GS_REF_NONE from the kernel's start.
     constexpr bool kSphLeaf = (FEAT & GS_FEAT_SPHLEAF) != 0;
@@ -2237,9 +2251,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 using mixed_t = std::integral_constant<bool, false>;
                 const bool lds_pass = (FEAT & GS_FEAT_LDSTREE) != 0 ||
                                       __builtin_amdgcn_ballot_w64(cur < THR_END && cur >= lim) == 0;
-                if (wave_fast && lds_pass && A.node_steps >= GS_NODE_STEPS) {
+                if (wave_fast && lds_pass && A.node_steps >= kUnroll) {
 #pragma unroll
-                    for (int nstep = 0; nstep < GS_NODE_STEPS; nstep++) node_step(fast_t{}, ldsp_t{});
+                    for (int nstep = 0; nstep < kUnroll; nstep++) node_step(fast_t{}, ldsp_t{});
                 } else if (wave_fast && lds_pass && A.node_steps == 1) {  // (trees of other-kind leaves, C3)
                     node_step(fast_t{}, ldsp_t{});
                 } else if (wave_fast && lds_pass) {
@@ -3946,6 +3960,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         ds->leaf_batch = GS_KIND_LEAF_BATCH;
         ds->shade_batch = GS_KIND_SHADE_BATCH;
         ds->node_steps = std::max<int32_t>(ds->node_steps, GS_KIND_NODE_STEPS);
+        if (ds->feat & GS_FEAT_NSPH) ds->node_steps = unroll_steps(ds->feat);  // (the unrolled pass, 16)
     }
     ds->tree = std::move(tree_keep);
     ds->pos = std::move(placed_pos);
@@ -3964,7 +3979,7 @@ gs_status gs_device_scene_info(const gs_device_scene* ds, gs_scene_info* out) {
     i.lds_leaves = ds->lds_leaves;
     i.lds_quads = ds->lds_quads;
     i.feat = ds->feat;
-    i.node_steps = std::max(1, std::min<int32_t>(GS_NODE_STEPS, g_node_steps > 0 ? g_node_steps : ds->node_steps));
+    i.node_steps = std::max(1, std::min<int32_t>(unroll_steps(ds->feat), g_node_steps > 0 ? g_node_steps : ds->node_steps));
     i.cert_boxes = ds->cert_boxes ? 1 : 0;
     i.nodes_per_leaf = ds->nodes_per_leaf;
     i.other_leaf_frac = ds->other_leaf_frac;
@@ -4229,7 +4244,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     a.cert_boxes = ds->cert_boxes ? 1 : 0;
     a.shade_batch = g_shade_batch > 0 ? g_shade_batch : ds->shade_batch;
     a.leaf_batch = std::max<int32_t>(1, g_leaf_batch > 0 ? g_leaf_batch : ds->leaf_batch);  // (0 would never step a node)
-    a.node_steps = std::max(1, std::min<int32_t>(GS_NODE_STEPS, g_node_steps > 0 ? g_node_steps : ds->node_steps));
+    a.node_steps = std::max(1, std::min<int32_t>(unroll_steps(ds->feat), g_node_steps > 0 ? g_node_steps : ds->node_steps));
     gs_device_scene* mds = const_cast<gs_device_scene*>(ds);
     std::lock_guard<std::mutex> lock(mds->mu);
     const bool chunked = kp.chunk != 0;
