@@ -61,12 +61,6 @@ using namespace gsd;
 #define GS_MIN_WAVES 4
 #endif
 #define GS_MAX_CHAIN 4
-// Device-only ref kind: a HittableList of consecutive quads, [first, first + count), first <
-// 2^22, count < 64 (index bits: first | count << 22).  0 disables the rewrite (A/B).
-#ifndef GS_QRUN
-#define GS_QRUN 0
-#endif
-#define DREF_QRUN 9u
 // Batch rounds (adaptive settings): whole-batch items only for batches up to this size
 #ifndef GS_ROUND_WHOLE_MAX_BATCH
 #define GS_ROUND_WHOLE_MAX_BATCH 256
@@ -76,9 +70,7 @@ using namespace gsd;
 #ifndef GS_NESTED_LDS
 #define GS_NESTED_LDS 1
 #endif
-#define QRUN_COUNT_SHIFT 22u
-#define QRUN_FIRST_MASK ((1u << QRUN_COUNT_SHIFT) - 1u)
-#define GS_NESTED_STACK 32  // max depth of a BVH under a Translate/RotateY chain (validation bound: the walk is stackless)
+#define GS_NESTED_STACK 32  // max depth of a BVH under a Translate/RotateY chain (a validation bound; the walk is stackless)
 // Kernel feature flags (template argument): scenes without them compile the code out.
 #define GS_FEAT_MEDIA 1   // ConstantMedium leaves (RNG draws inside traversal)
 #define GS_FEAT_NESTED 2  // BVHs under Translate/RotateY (a second-level threaded walk)
@@ -303,23 +295,11 @@ __device__ __forceinline__ double lo_hi(unsigned int lo, unsigned int hi) { retu
 
 // A node record (2 x 16 B) at byte offset `off`: a = (mnx, mny, mxx, mxy), b = (mnz, mxz,
 // hit, miss).  (Offsets are u32: fewer than 2^26 records; leaf offsets i * 48 < 2^32.)
-//
-// Bank swizzle (GS_NODE_SWZ).  ds_read_b128 serves a wave in 4 groups of 16 lanes, each
-// lane's 16 B on 4 of the 64 banks, (a / 16) mod 16 picking the 4 (MI355X_MICROARCH.md,
-// LDS): with 32-B records every lane's first half lies on an even 4-bank group, so 16
-// lanes at different records share 8 groups.  The mirror stores an odd record's halves
-// swapped and a node link is the address of its record's first half (index << 5, plus 16
-// for an odd index): the first reads then spread over all 16 groups, and the second half
-// is at link ^ 16.  Global records keep their order (link & ~31).
-#ifndef GS_NODE_SWZ
-#define GS_NODE_SWZ 0  // measured: C4 -1.4%, C3 +0.7%, C5 -0.7% (profiles/r03/ab_node_swizzle_flush_rank.txt)
-#endif
-#ifndef GS_QUAD_SWZ
-#define GS_QUAD_SWZ 0  // measured: final_scene +0.2%, C3 +0.5%, C5 -1.3% (profiles/r03/ab_quad_swizzle.txt)
-#endif
-__host__ __device__ constexpr uint32_t node_link(uint32_t pos) { return (pos << 5) | (GS_NODE_SWZ ? (pos & 1u) << 4 : 0u); }
-__device__ __forceinline__ uint32_t node_half_b(uint32_t off) { return GS_NODE_SWZ ? off ^ 16u : off + 16u; }
-__device__ __forceinline__ uint32_t node_global(uint32_t off) { return GS_NODE_SWZ ? off & ~31u : off; }
+// (Bank-swizzled node and quad records were measured and dropped in round 3: C4 -1.4%,
+// C5 -1.3%)
+__host__ __device__ constexpr uint32_t node_link(uint32_t pos) { return pos << 5; }
+__device__ __forceinline__ uint32_t node_half_b(uint32_t off) { return off + 16u; }
+__device__ __forceinline__ uint32_t node_global(uint32_t off) { return off; }
 template <bool LDS_ONLY>
 __device__ __forceinline__ void load_tnode(const uint8_t* s_nodes, const TNode* g, uint32_t off, uint32_t lds_bytes,
                                            u32x4& a, u32x4& b) {
@@ -353,9 +333,7 @@ __device__ __forceinline__ void load_tnode_w(const uint8_t* s_nodes, const TNode
 // registers live across the whole loop: recomputed where needed, they cost nothing in
 // the common path.
 __device__ __forceinline__ d3 inv_of(d3 d) {
-#ifndef GS_NO_INV_BARRIER
     asm volatile("" : "+v"(d.x), "+v"(d.y), "+v"(d.z));
-#endif
     return mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
 }
 // A leaf record: the sphere's centre and radius, its next link and its ABI ref.
@@ -470,148 +448,24 @@ __device__ __forceinline__ DNode ld_node_g(const DNode* p) {  // a nested-BVH no
 }
 template <bool UNI>
 __device__ __forceinline__ u32x4 quad_part(const QuadSrc& qs, uint32_t i, uint32_t k) {
-    // (the mirror stores quad i's 16-B chunk k at chunk k ^ (i & 7): 128-B records would put
-    // every lane's chunk k on the same 2 of ds_read_b128's 16 bank groups, GS_NODE_SWZ)
-    if (!UNI && i < qs.n_lds)
-        return *(lds_u32x4*)(qs.lds + i * (uint32_t)sizeof(TQuad) + ((GS_QUAD_SWZ ? (k ^ (i & 7u)) : k) << 4));
+    if (!UNI && i < qs.n_lds) return *(lds_u32x4*)(qs.lds + i * (uint32_t)sizeof(TQuad) + (k << 4));
     return sp<UNI>(reinterpret_cast<const u32x4*>(qs.g + i))[k];
 }
-// Axis-aligned quads (GS_AQUAD; every Quad::cube face, quad.rs:54-80, the Cornell walls,
-// the lights): the plane's normal is +-e_a and u, v each have one non-zero component, on
-// the two other axes iu, iv.  Every term of the reference's dot and cross products that
-// multiplies a zero component is then a zero, and adding a zero to a non-zero value is
-// exact, so Quad::hit's values reduce to (TQuad's aligned form, set up by aligned_tquad):
-//   t     = (D' - o_a) / d_a                        (D' = n_a D; plane.rs:21-29, |den| = |d_a|)
-//   alpha = W' (p_iu V_iv),  beta = W' (U_iu p_iv)  (W' = +-w_a: the cross products' sign)
-//   p_k   = (o_k + d_k t) - Q_k                     (ray.at(t) - q, quad.rs:86-88)
-// with the same roundings as the full test: the same t, alpha and beta, bit for bit,
-// except that where the full test's value is a zero its sign may differ -- no comparison
-// (0 <= alpha, tmin <= t) and no later use tells a zero's sign apart.  The record's first
-// word is a signalling-NaN tag (no arithmetic result, and the host re-tags a full record
-// that would collide) carrying the axes: code = 2 a + o, o = 0: (iu, iv) = (a+1, a+2) mod
-// 3, o = 1: the other order.  Layout: [tag|code, D'], [Q_iu, Q_iv], [U_iu, V_iv], [W', 0].
-#ifndef GS_AQUAD
-#define GS_AQUAD 0  // single quads in the aligned form (dynamic selects: measured slower, profiles/r04/ab_aligned_quads.txt)
-#endif
-#ifndef GS_AQ_UNIFORM
-#define GS_AQ_UNIFORM 0  // 1: a wave-uniform axis code runs a compile-time copy (no selects)
-#endif
+// The aligned form's tag (aligned_tquad, host: the cube records' derivation): a
+// signalling-NaN first word carrying the axis code 2 a + o.  (Single quads in the aligned
+// form, with per-lane selects or compile-time copies per axis code, were measured and
+// dropped in round 4, profiles/r04/ab_aligned_quads.txt.)
 #define GS_AQ_TAG 0xFFF4A5C0u
-template <bool UNI, class Pick>
-__device__ __forceinline__ bool aquad_accept(const QuadSrc& qs, uint32_t i, double Dp, Pick pick, double tmin,
-                                             double tmax, double& t_out) {
-    double oa, da, ou, du, ov, dv;
-    pick(oa, da, ou, du, ov, dv);
-    if (fabs(da) < 1e-8) return false;
-    const double t = (Dp - oa) / da;
-    if (!(tmin <= t && t <= tmax)) return false;
-    const u32x4 b = quad_part<UNI>(qs, i, 1), c = quad_part<UNI>(qs, i, 2), e = quad_part<UNI>(qs, i, 3);
-    const double pu = (ou + du * t) - lo_hi(b.x, b.y);
-    const double pv = (ov + dv * t) - lo_hi(b.z, b.w);
-    const double W = lo_hi(e.x, e.y);
-    const double alpha = W * (pu * lo_hi(c.z, c.w));
-    const double beta = W * (lo_hi(c.x, c.y) * pv);
-    if (!(0.0 <= alpha && alpha <= 1.0) || !(0.0 <= beta && beta <= 1.0)) return false;
-    t_out = t;
-    return true;
-}
-__device__ __forceinline__ double d3_at(const d3& v, uint32_t k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
 template <int CODE>
 __device__ __forceinline__ double d3_c(const d3& v, int which) {  // which: 0 = a, 1 = iu, 2 = iv
     constexpr int A = CODE >> 1, O = CODE & 1;
     const int k = which == 0 ? A : (which == 1 ? (A + 1 + O) % 3 : (A + 2 - O) % 3);
     return k == 0 ? v.x : (k == 1 ? v.y : v.z);
 }
-template <bool UNI, int CODE>
-__device__ __forceinline__ bool aquad_fixed(const QuadSrc& qs, uint32_t i, double Dp, const Ray& ray, double tmin,
-                                            double tmax, double& t_out) {
-    return aquad_accept<UNI>(
-        qs, i, Dp,
-        [&](double& oa, double& da, double& ou, double& du, double& ov, double& dv) {
-            oa = d3_c<CODE>(ray.o, 0);
-            da = d3_c<CODE>(ray.d, 0);
-            ou = d3_c<CODE>(ray.o, 1);
-            du = d3_c<CODE>(ray.d, 1);
-            ov = d3_c<CODE>(ray.o, 2);
-            dv = d3_c<CODE>(ray.d, 2);
-        },
-        tmin, tmax, t_out);
-}
 template <bool UNI>
 __device__ __forceinline__ bool quad_test(const QuadSrc& qs, uint32_t i, const Ray& ray, double tmin, double tmax,
                                           double& t_out) {
     const u32x4 a = quad_part<UNI>(qs, i, 0);
-#if GS_AQUAD
-    if ((a.y & ~7u) == GS_AQ_TAG) {
-        const uint32_t code = a.y & 7u;
-        const double Dp = lo_hi(a.z, a.w);
-#if GS_AQ_UNIFORM == 2
-        // Waterfall over the wave's axis codes (one in a box list's lockstep walk, where
-        // every lane is at the same face of its box): the lanes of the first remaining code
-        // copy their ray's components under a scalar branch (register moves, no selects),
-        // then run the one copy of the test.
-        bool res = false;
-#pragma unroll 1
-        for (;;) {
-            const uint32_t c0 = UNI ? code : __builtin_amdgcn_readfirstlane(code);
-            if (code == c0) {
-                double oa, da, ou, du, ov, dv;
-#define GS_AQ_CASE(C)                                                                       \
-    case C:                                                                                 \
-        __asm__ volatile("" ::: "memory");                                                  \
-        oa = d3_c<C>(ray.o, 0), da = d3_c<C>(ray.d, 0), ou = d3_c<C>(ray.o, 1);           \
-        du = d3_c<C>(ray.d, 1), ov = d3_c<C>(ray.o, 2), dv = d3_c<C>(ray.d, 2);           \
-        break;
-                switch (c0) {
-                    GS_AQ_CASE(0)
-                    GS_AQ_CASE(1)
-                    GS_AQ_CASE(2)
-                    GS_AQ_CASE(3)
-                    GS_AQ_CASE(4)
-                    default:
-                    GS_AQ_CASE(5)
-                }
-#undef GS_AQ_CASE
-                res = aquad_accept<UNI>(
-                    qs, i, Dp,
-                    [&](double& a0, double& a1, double& a2, double& a3, double& a4, double& a5) {
-                        a0 = oa, a1 = da, a2 = ou, a3 = du, a4 = ov, a5 = dv;
-                    },
-                    tmin, tmax, t_out);
-                break;
-            }
-        }
-        return res;
-#elif GS_AQ_UNIFORM
-        const uint32_t c0 = __builtin_amdgcn_readfirstlane(code);
-        if (UNI || __builtin_amdgcn_ballot_w64(code != c0) == 0) {
-            switch (c0) {
-                case 0: return aquad_fixed<UNI, 0>(qs, i, Dp, ray, tmin, tmax, t_out);
-                case 1: return aquad_fixed<UNI, 1>(qs, i, Dp, ray, tmin, tmax, t_out);
-                case 2: return aquad_fixed<UNI, 2>(qs, i, Dp, ray, tmin, tmax, t_out);
-                case 3: return aquad_fixed<UNI, 3>(qs, i, Dp, ray, tmin, tmax, t_out);
-                case 4: return aquad_fixed<UNI, 4>(qs, i, Dp, ray, tmin, tmax, t_out);
-                default: return aquad_fixed<UNI, 5>(qs, i, Dp, ray, tmin, tmax, t_out);
-            }
-        }
-#endif
-        const uint32_t ax = code >> 1, o = code & 1u;
-        const uint32_t k1 = ax == 2u ? 0u : ax + 1u, k2 = ax == 0u ? 2u : ax - 1u;  // a+1, a+2 (mod 3)
-        return aquad_accept<UNI>(
-            qs, i, Dp,
-            [&](double& oa, double& da, double& ou, double& du, double& ov, double& dv) {
-                oa = d3_at(ray.o, ax);
-                da = d3_at(ray.d, ax);
-                const double o1 = d3_at(ray.o, k1), o2 = d3_at(ray.o, k2);
-                const double d1 = d3_at(ray.d, k1), d2 = d3_at(ray.d, k2);
-                ou = o ? o2 : o1;
-                ov = o ? o1 : o2;
-                du = o ? d2 : d1;
-                dv = o ? d1 : d2;
-            },
-            tmin, tmax, t_out);
-    }
-#endif
     const u32x4 b = quad_part<UNI>(qs, i, 1);
     return quad_accept_plane(
         mk(lo_hi(a.x, a.y), lo_hi(a.z, a.w), lo_hi(b.x, b.y)), lo_hi(b.z, b.w),
@@ -713,15 +567,6 @@ __device__ __forceinline__ void chain_count(const DevScene& sc, uint32_t cur, un
 // [x0 y0 z0 x1 y1 z1 dx dy dz w_xy w_zy w_xz] (a negation is exact and free, an f64
 // operand modifier).  The host (cube_record) builds a cube only when all six faces' aligned
 // records equal what this table derives; the other lists keep the loop.
-#ifndef GS_CUBE
-#define GS_CUBE 1
-#endif
-#ifndef GS_CUBE_LDS
-#define GS_CUBE_LDS 1  // mirror a prefix of the cube records in LDS (after the other mirrors)
-#endif
-#ifndef GS_CUBE_ORDER
-#define GS_CUBE_ORDER 0  // 1: largest boxes first; measured neutral on final_scene (profiles/r04/ab_cube_order.txt)
-#endif
 #define GS_CUBE_FLAG 0x80000000u
 #define GS_CUBE_DOUBLES 12
 __host__ __device__ constexpr int cube_code(int k) { return k == 0 || k == 2 ? 4 : (k == 1 || k == 3 ? 1 : 3); }
@@ -731,24 +576,11 @@ __host__ __device__ constexpr int cube_src(int k, int f) {
                              {0, 2, 1, 8, 7, 10},   {4, 0, 5, 6, -8, -11}, {1, 0, 2, 6, 8, 11}};
     return t[k][f];
 }
-#ifndef GS_CUBE_LAZY
-#define GS_CUBE_LAZY 0  // 1: each face reads the values it needs when it needs them; 0: all 12 first
-#endif
-struct CubeRegs {  // the record read up front
+// (the record is read up front: faces reading their values lazily measured -0.3 to -2.8%)
+struct CubeRegs {
     double c[GS_CUBE_DOUBLES];
     template <int J>
     __device__ __forceinline__ double get() const { return c[J]; }
-};
-template <bool UNI>
-struct CubeLazy {  // the record where it lies: the LDS mirror or global memory
-    const uint8_t* lds;
-    const double* g;
-    bool in_lds;
-    template <int J>
-    __device__ __forceinline__ double get() const {
-        if (!UNI && in_lds) return *(const __attribute__((address_space(3))) double*)(uintptr_t)(lds + 8 * J);
-        return *sp<UNI>(g + J);
-    }
 };
 template <bool UNI>
 __device__ __forceinline__ u32x4 cube_part(const QuadSrc& qs, const double* g, uint32_t cube, uint32_t k, bool lds) {
@@ -795,10 +627,6 @@ __device__ __forceinline__ void cube_test(const DevScene& sc, const QuadSrc& qs,
                                           const Ray& r, double tmin, uint32_t inst_ref, LeafHit& res,
                                           unsigned long long* cnt) {
     atomicAdd(&cnt[C_QUAD], 6ull);
-#if GS_CUBE_LAZY
-    const CubeLazy<UNI> c{qs.lcubes + cube * (uint32_t)(GS_CUBE_DOUBLES * 8), sc.cubes + (size_t)cube * GS_CUBE_DOUBLES,
-                          cube < qs.n_lcubes};
-#else
     CubeRegs c;
     // the LDS copy when every lane's cube is mirrored (a wave-uniform choice: a per-lane
     // one ran both kinds of loads under masks, final_scene -2.3%), else global for all
@@ -809,52 +637,24 @@ __device__ __forceinline__ void cube_test(const DevScene& sc, const QuadSrc& qs,
         c.c[2 * k] = lo_hi(v.x, v.y);
         c.c[2 * k + 1] = lo_hi(v.z, v.w);
     }
-#endif
     cube_faces(c, q0, r, tmin, inst_ref, res);
 }
 
 // A HittableList (hittable.rs:71-86: shrinking closest) or one primitive.
-// A device-side QRUN ref (DREF_QRUN, set at upload: render.hip qrun_ref) is a list whose
-// members are the quads [first, first + count) in order (every Quad::cube, quad.rs:54-80),
-// so neither the list record nor its member refs are read: the same quads in the same order.
-// QR: this call site may meet QRUN refs (top-level and nested leaves, instance chains that
-// end in a list; not medium boundaries, which the host leaves as plain lists).
-template <bool UNI, bool QR = true>
+template <bool UNI>
 __device__ __forceinline__ void shape_test(const DevScene& sc, const QuadSrc& qs, uint32_t cur, const Ray& r,
                                            double tmin, double closest, uint32_t inst_ref, LeafHit& res,
                                            unsigned long long* cnt) {
-#if GS_QRUN
-    const uint32_t kind = cur >> GS_REF_SHIFT;
-    if (kind == GS_REF_LIST || (QR && kind == DREF_QRUN)) {
-        atomicAdd(&cnt[C_LIST], 1ull);
-        const bool direct = QR && kind == DREF_QRUN;
-        gs_list l;
-        if (direct) {
-            l.first = cur & QRUN_FIRST_MASK;
-            l.count = (cur & GS_REF_MASK) >> QRUN_COUNT_SHIFT;
-        } else {
-            l = ld_list<UNI>(sc.lists + (cur & GS_REF_MASK));
-            if (GS_CUBE && (l.count & GS_CUBE_FLAG)) {
-                cube_test<UNI>(sc, qs, l.first, l.count & ~GS_CUBE_FLAG, r, tmin, inst_ref, res, cnt);
-                return;
-            }
-        }
-#pragma unroll 1
-        for (uint32_t k = 0; k < l.count; k++)
-            prim_test<UNI>(sc, qs, direct ? GS_MAKE_REF(GS_REF_QUAD, l.first + k) : ld_u32<UNI>(sc.list_refs + l.first + k),
-                           r, tmin, res.t, inst_ref, res, cnt);
-#else
     if ((cur >> GS_REF_SHIFT) == GS_REF_LIST) {
         atomicAdd(&cnt[C_LIST], 1ull);
         const gs_list l = ld_list<UNI>(sc.lists + (cur & GS_REF_MASK));
-        if (GS_CUBE && (l.count & GS_CUBE_FLAG)) {
+        if (l.count & GS_CUBE_FLAG) {
             cube_test<UNI>(sc, qs, l.first, l.count & ~GS_CUBE_FLAG, r, tmin, inst_ref, res, cnt);
         } else {
 #pragma unroll 1
             for (uint32_t k = 0; k < l.count; k++)
                 prim_test<UNI>(sc, qs, ld_u32<UNI>(sc.list_refs + l.first + k), r, tmin, res.t, inst_ref, res, cnt);
         }
-#endif
     } else {
         prim_test<UNI>(sc, qs, cur, r, tmin, closest, inst_ref, res, cnt);
     }
@@ -888,7 +688,7 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
     b1.t = DMAX;
     Ray rb = r;
     const uint32_t shape = walk_chain<UNI>(sc, md.boundary, rb, cnt);
-    shape_test<UNI, false>(sc, qs, shape, rb, -DMAX, DMAX, GS_REF_NONE, b1, cnt);
+    shape_test<UNI>(sc, qs, shape, rb, -DMAX, DMAX, GS_REF_NONE, b1, cnt);
     if (!b1.hit) return;
     if constexpr (REUSE) {
         chain_count<UNI>(sc, md.boundary, cnt);
@@ -899,7 +699,7 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
     LeafHit b2;
     b2.hit = false;
     b2.t = DMAX;
-    shape_test<UNI, false>(sc, qs, shape, rb, b1.t + 0.0001, DMAX, GS_REF_NONE, b2, cnt);
+    shape_test<UNI>(sc, qs, shape, rb, b1.t + 0.0001, DMAX, GS_REF_NONE, b2, cnt);
     if (!b2.hit) return;
     double t1 = b1.t, t2 = b2.t;
     if (t1 < tmin) t1 = tmin;
@@ -932,12 +732,6 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
 // box of balls, main.rs:741-755; GS_FEAT_NSPH), Sphere::hit directly, with no kind
 // dispatch; else the generic test.  (A runtime branch between the two, and |d|^2 hoisted
 // out of the walk, spilled 8-16 B/lane.)
-#ifndef GS_NRAD_UNIFORM
-#define GS_NRAD_UNIFORM 1
-#endif
-#ifndef GS_NESTED_LANE_COUNT
-#define GS_NESTED_LANE_COUNT 1
-#endif
 template <bool SPH, bool LC>
 __device__ __forceinline__ void nested_leaf(const DevScene& sc, const QuadSrc& qs, const u32x4& a, const u32x4& b,
                                             const Ray& r, double tmin, double closest, uint32_t inst_ref, LeafHit& res,
@@ -948,14 +742,10 @@ __device__ __forceinline__ void nested_leaf(const DevScene& sc, const QuadSrc& q
         // in the scene's radius table in the ref's kind bits (the kind is a sphere here)
         if constexpr (LC) n_sph++;
         else atomicAdd(&cnt[C_SPH], 1ull);
-#if GS_NRAD_UNIFORM
         // (a wave whose lanes share the radius slot -- one radius in the scene: always --
         // reads it with a scalar load)
         const uint32_t slot = b.w >> GS_REF_SHIFT, s0 = __builtin_amdgcn_readfirstlane(slot);
         const double rad = __builtin_amdgcn_ballot_w64(slot != s0) == 0 ? sp<true>(sc.nradii)[s0] : sp<false>(sc.nradii)[slot];
-#else
-        const double rad = sp<false>(sc.nradii)[b.w >> GS_REF_SHIFT];
-#endif
         double t;
         if (sphere_accept(mk(lo_hi(a.x, a.y), lo_hi(a.z, a.w), lo_hi(b.x, b.y)), rad, r, len2(r.d), tmin, closest, t)) {
             res.hit = true;
@@ -967,9 +757,6 @@ __device__ __forceinline__ void nested_leaf(const DevScene& sc, const QuadSrc& q
         shape_test<false>(sc, qs, b.w, r, tmin, closest, inst_ref, res, cnt);
     }
 }
-#ifndef GS_NESTED_WW
-#define GS_NESTED_WW 0  // 1: measured neutral on final_scene (2 142 vs 2 155, profiles/r04/ab_cube_records.txt)
-#endif
 template <bool SPH, bool LC>
 __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs, uint32_t root, const Ray& r, double tmin,
                                            double closest, uint32_t inst_ref, LeafHit& res,
@@ -992,48 +779,8 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
         if constexpr (LC) n_nodes++;
         else atomicAdd(&cnt[C_NODES], 1ull);
     };
-#if GS_NESTED_WW
-    // "while-while": node steps until every lane of the walk sits at a leaf or has ended,
-    // then the leaf lanes test their leaves together (a sphere test costs several node
-    // steps: with one loop, an iteration whose lanes were at both kinds paid for both).
-    // Each lane's records, order and results are those of the single loop.
-#pragma unroll 1
-    while (cur != THR_END) {
-        u32x4 a, b;
-#pragma unroll 1
-        for (;;) {
-            // (a scalar branch to the LDS reads when every active lane's record is mirrored)
-            if (__builtin_amdgcn_ballot_w64(cur >= qs.n_nlds) == 0) {
-                a = *(lds_u32x4*)(qs.nlds + cur * 32u);
-                b = *(lds_u32x4*)(qs.nlds + cur * 32u + 16u);
-            } else {
-                const u32x4* q = sp<false>(reinterpret_cast<const u32x4*>(sc.nrecs + cur));
-                a = q[0];
-                b = q[1];
-            }
-            if (b.z & NREC_LEAF) break;
-            count_node();
-            bool h = false, undecided = true;
-            if (fast)
-                h = box_cert(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(b.x), __uint_as_float(a.z),
-                             __uint_as_float(a.w), __uint_as_float(b.y), c, 0.001f, closest32, undecided);
-            if (undecided) h = box_hit_v(ld_node_g(sc.nodes + cur), r.o, inv_of(r.d), tmin, closest);
-#ifdef GS_CERT_CHECK
-            if (fast && !undecided && box_hit_v(ld_node_g(sc.nodes + cur), r.o, inv_of(r.d), tmin, closest) != h)
-                atomicAdd(&cnt[15], 1ull);
-#endif
-            cur = h ? b.z : b.w;
-            if (cur == THR_END) break;
-        }
-        if (cur == THR_END) break;
-        nested_leaf<SPH, LC>(sc, qs, a, b, r, tmin, closest, inst_ref, res, cnt, n_sph);
-        if (res.hit) {  // res.t only ever shrinks
-            closest = res.t;
-            closest32 = (float)res.t;
-        }
-        cur = b.z & ~NREC_LEAF;
-    }
-#else
+    // (the walk as while-while -- node steps until every lane is at a leaf, then the leaves
+    // together -- measured neutral on final_scene)
 #pragma unroll 1
     while (cur != THR_END) {
         u32x4 a, b;
@@ -1069,7 +816,6 @@ __device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs
             cur = h ? b.z : b.w;
         }
     }
-#endif
     if constexpr (LC) {
         atomicAdd(&cnt[C_NODES], (unsigned long long)n_nodes);
         if constexpr (SPH) atomicAdd(&cnt[C_SPH], (unsigned long long)n_sph);
@@ -1098,7 +844,7 @@ __device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, const QuadSrc& qs,
         medium_test<UNI, (FEAT & GS_FEAT_NESTED) == 0>(sc, qs, cur, r, tmin, closest, inst_ref, rng, res, cnt);
     } else if ((FEAT & GS_FEAT_NESTED) && (cur >> GS_REF_SHIFT) == GS_REF_NODE) {
         nested_bvh<(FEAT & GS_FEAT_NSPH) != 0,
-                   GS_NESTED_LANE_COUNT && (FEAT & (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)) != (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)>(
+                   (FEAT & (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)) != (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)>(
             sc, qs, cur & GS_REF_MASK, r, tmin, closest, inst_ref, res, cnt);
     } else {
         shape_test<UNI>(sc, qs, cur, r, tmin, closest, inst_ref, res, cnt);
@@ -1239,12 +985,9 @@ __device__ GS_NOINLINE d3 texture_value(const DevScene& sc, uint32_t tex, double
 __device__ __forceinline__ d3 hdri_texel(const DevScene& sc, d3 rot, unsigned long long* cnt) {
     const gs_background& bg = sc.bg;
     uint32_t x, y;
-#ifndef GS_SKY_CERT
-#define GS_SKY_CERT 1
-#endif
     // f32 angles where they certify the texel, else the reference's f64 atan2 / asin
     // (sky_index_f32 / sky_index_f64, geometry.hpp)
-    if (!GS_SKY_CERT || !sky_index_f32(rot, bg.width, bg.height, x, y)) sky_index_f64(rot, bg.width, bg.height, x, y);
+    if (!sky_index_f32(rot, bg.width, bg.height, x, y)) sky_index_f64(rot, bg.width, bg.height, x, y);
     const uint64_t k = y * (uint64_t)bg.width + x;
     atomicAdd(&cnt[C_HDRI], 1ull);
     if (sc.hdri_rgbe) {
@@ -1535,6 +1278,10 @@ __device__ GS_NOINLINE Scatter scatter(const DevScene& sc, HitRec h, d3 in_dir, 
 // The placement pilot's count (GS_FEAT_VISITS): one atomic per distinct record among the
 // wave's active lanes (every ray of a pilot tests the root and the records below it: one
 // atomic per lane on those addresses serialised the pilot, 111 ms on MI355X C4).
+// The lead lane is retired every round whatever the ballot returns, so the loop ends
+// after at most 64 rounds even if the mask it starts from held a lane that is not active
+// here (the round-3 stamps-build hang: DESIGN.md §7); a lane outside `same` but in `m`
+// is then counted by nobody, which the pilot's tests would show as a miscount.
 __device__ __forceinline__ void count_visit(uint32_t* counts, uint32_t idx) {
     uint64_t m = __builtin_amdgcn_ballot_w64(true);
 #pragma unroll 1
@@ -1551,10 +1298,7 @@ __device__ __forceinline__ void count_visit(uint32_t* counts, uint32_t idx) {
 // phases, written to their own debug buffer (the d_item_visits pointer, reinterpreted
 // as u64[3]) — never to an output.  The stamps' fences perturb scheduling, so only the
 // shares are meaningful, not the absolute time.
-#if defined(GS_STAMPS) && defined(GS_STAMP_NOTIME)  // (hang probe: the stamps build without its clock reads)
-#define GS_STAMP(t) do { t = 0; } while (0)
-#define GS_REGION(k, t0) do { } while (0)
-#elif defined(GS_STAMPS)
+#if defined(GS_STAMPS)
 #define GS_STAMP(t) do { __builtin_amdgcn_sched_barrier(0); t = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 // Region timing inside divergent shading code: the first active lane adds the wave's
 // elapsed clock to its wave's LDS slot (one count per wave, whatever the mask).
@@ -1597,12 +1341,9 @@ enum { L_ND_CHUNKED = L_LSUM };
 // Media / nested-BVH kernels keep the path throughput (Tr, Tg, Tb: read and written only
 // by the shade pass) in three more f64 lane fields (before those), out of the registers their
 // leaf tests need (round 3: with them in VGPRs these instantiations spilled 52-76 B/lane).
-#ifndef GS_T_LDS
-#define GS_T_LDS 1
-#endif
 // (not the placement pilot's counting kernel: it launches with the scene's own lane layout)
 __host__ __device__ constexpr bool t_in_lds(int feat) {
-    return GS_T_LDS && (feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED)) != 0 && (feat & GS_FEAT_VISITS) == 0;
+    return (feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED)) != 0 && (feat & GS_FEAT_VISITS) == 0;
 }
 __host__ __device__ constexpr uint32_t lane_nd(bool chunked, int feat) {
     return (chunked ? (uint32_t)L_ND_CHUNKED : (uint32_t)L_ND) + (t_in_lds(feat) ? 3u : 0u);
@@ -1634,14 +1375,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     {
         const uint4* src = reinterpret_cast<const uint4*>(A.tnodes);
         uint4* dst = reinterpret_cast<uint4*>(s_nodes);
-        // (record r's 16-B halves: swapped when r is odd, GS_NODE_SWZ)
-        for (uint32_t k = threadIdx.x; k < A.lds_nodes * 2u; k += GS_BLOCK) dst[GS_NODE_SWZ ? k ^ ((k >> 1) & 1u) : k] = src[k];
+        for (uint32_t k = threadIdx.x; k < A.lds_nodes * 2u; k += GS_BLOCK) dst[k] = src[k];
         src = reinterpret_cast<const uint4*>(A.tleaves);
         dst = reinterpret_cast<uint4*>(s_leaves);
         for (uint32_t k = threadIdx.x; k < A.lds_leaves * 3u; k += GS_BLOCK) dst[k] = src[k];
         src = reinterpret_cast<const uint4*>(A.tquads);
         dst = reinterpret_cast<uint4*>(s_quads);
-        for (uint32_t k = threadIdx.x; k < A.lds_quads * 8u; k += GS_BLOCK) dst[GS_QUAD_SWZ ? k ^ ((k >> 3) & 7u) : k] = src[k];
+        for (uint32_t k = threadIdx.x; k < A.lds_quads * 8u; k += GS_BLOCK) dst[k] = src[k];
         if constexpr ((FEAT & GS_FEAT_NESTED) != 0) {
             src = reinterpret_cast<const uint4*>(A.nrecs);
             dst = reinterpret_cast<uint4*>(s_quads + (size_t)A.lds_quads * sizeof(TQuad));
@@ -1672,11 +1412,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     const uint32_t tid = threadIdx.x;
     const uint64_t flushers = __builtin_amdgcn_ballot_w64(tid < GS_CNT_SLOTS);  // the counters' flushing lanes
     const double tmin = 0.001;
-#ifndef GS_NESTED_SITES
-#define GS_NESTED_SITES 1
-#endif
     // BVHs under instances keep round 1's advance / begin_ray sites (see the shade pass)
-    constexpr bool kOldSites = GS_NESTED_SITES && (FEAT & GS_FEAT_NESTED) != 0;
+    constexpr bool kOldSites = (FEAT & GS_FEAT_NESTED) != 0;
     constexpr int kUnroll = unroll_steps(FEAT);  // node steps of an unrolled node pass
     // Every top-level leaf a stationary sphere: no instance is ever hit, so the hit's
     // instance (lane state L_HINST) stays GS_REF_NONE from the kernel's start.
@@ -1717,14 +1454,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     bool fresh = false;
     // hot counters kept in registers, flushed per pixel
     uint32_t c_nodes = 0, c_sph = 0;  // (per lane: one VALU add beat a 64-bit SALU wave count)
-    // GS_SALU_COUNT: node visits counted per wave on the scalar unit (popcount of the step's
-    // lane mask), not per lane on the VALU -- the kernel's VALU is ~88% busy.
-    // Launches that need per-pixel counts (item_visits) run the pilot's instantiation.
-#ifndef GS_SALU_COUNT
-#define GS_SALU_COUNT 0
-#endif
-    constexpr bool kSaluCount = GS_SALU_COUNT && (FEAT & GS_FEAT_VISITS) == 0;
-    uint64_t w_nodes = 0;
 
     auto begin_ray = [&]() {
         // AABB::hit's `1.0 / ray.direction[axis]` (AABB.rs:64), hoisted per ray (same value)
@@ -1777,7 +1506,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     // a stationary-sphere test: a lane count (flushed with c_nodes), or in t_in_lds kernels
     // a wave-aggregated LDS atomic, as prim_test counts the other kinds (no register kept)
     auto count_sph = [&]() __attribute__((always_inline)) {
-        if constexpr (kTLds || kSaluCount) atomicAdd(&s_cnt[C_SPH], 1ull);
+        if constexpr (kTLds) atomicAdd(&s_cnt[C_SPH], 1ull);
         else c_sph++;
     };
     auto end_chunk = [&]() {
@@ -1794,10 +1523,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             flush_counts();
         }
 #endif
-#ifndef GS_FLUSH_PER_ITEM
-#define GS_FLUSH_PER_ITEM 0
-#endif
-        if (GS_FLUSH_PER_ITEM || (c_nodes | c_sph) >= (1u << 30)) flush_counts();
+        if ((c_nodes | c_sph) >= (1u << 30)) flush_counts();
         st = S_NEED;
     };
 
@@ -2106,11 +1832,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         // shade count and the slab flavour are wave-uniform SGPR facts: no per-iteration
         // ballot for the former, a scalar branch (no exec-mask juggling) for the latter.
         const uint64_t alive = __builtin_amdgcn_ballot_w64(st != S_DONE);
-#ifdef GS_NO_CERT
-        const bool wave_fast = false;
-#else
         const bool wave_fast = __builtin_amdgcn_ballot_w64(st == S_TRACE && !fast) == 0;
-#endif
         // Invariant: cur != THR_END exactly for lanes whose ray is still being traced
         // (every other lane holds THR_END), so the loop reads lane states from `cur` alone
         // and only marks finished lanes S_SHADE once it ends.
@@ -2165,7 +1887,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 auto node_step = [&](auto fast_tag, auto ldsp_tag) __attribute__((always_inline)) {
                 constexpr bool FAST = decltype(fast_tag)::value;
                 constexpr bool LDSP = decltype(ldsp_tag)::value;
-#if defined(GS_STAMPS) && !defined(GS_STAMP_NOPASS)
+#ifdef GS_STAMPS
                 {
                     const bool glob = !((FEAT & GS_FEAT_LDSTREE) != 0) && cur < THR_END && cur >= (A.lds_nodes << 5);
                     const uint64_t act = __builtin_amdgcn_ballot_w64(LDSP ? cur < lim : cur < THR_END);
@@ -2176,7 +1898,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     d_wlanes += (uint64_t)__popcll(act);
                 }
 #endif
-                if constexpr (kSaluCount) w_nodes += (uint64_t)__popcll(__builtin_amdgcn_ballot_w64(LDSP ? cur < lim : cur < THR_END));
                 if (__builtin_expect(LDSP ? cur < lim : cur < THR_END, 1)) {
                     // One 32-B record (2 x 16 B; from LDS, offset = cur, or off the SGPR
                     // base), the box test, and the next record: the hit link or the miss link.
@@ -2187,7 +1908,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     } else {
                         load_tnode_w<(FEAT & GS_FEAT_LDSTREE) != 0>(s_nodes, A.tnodes, cur, A.lds_nodes << 5, ra, rb);
                     }
-                    if constexpr (!kSaluCount) c_nodes++;
+                    c_nodes++;
                     if constexpr ((FEAT & GS_FEAT_VISITS) != 0) {
                         if (P->visits) count_visit(P->visits, cur >> 5);
                     }
@@ -2231,13 +1952,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         cur = h ? rb.z : rb.w;
                         GS_MARK("slow_end");
                     }
-#ifdef GS_PAD_NODE  // calibration builds: GS_PAD_NODE extra f32 VALU ops per node step
-                    {
-                        float pad = __uint_as_float(ra.x);
-#pragma unroll
-                        for (int q = 0; q < GS_PAD_NODE; q++) asm volatile("v_add_f32 %0, %0, %0" : "+v"(pad));
-                    }
-#endif
                 }
                 };
                 // The scene's step count (gs_device_scene.node_steps): the full count as one
@@ -2297,7 +2011,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 if constexpr ((FEAT & GS_FEAT_VISITS) != 0) {
                     if (P->visits) count_visit(P->visits, P->visit_leaf_base + (cur & ~THR_LEAF));
                 }
-#if defined(GS_STAMPS) && !defined(GS_STAMP_NOPASS)
+#ifdef GS_STAMPS
                 {  // counted by the pass's first active lane (summed over lanes at the end)
                     // The r03 hang of this build on media scenes was in these counts.  Round-4
                     // probes (profiles/r04/stamps_hang_probes.txt): waiting for every load first
@@ -2340,10 +2054,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                     GS_MARK("sphere_end");
                 };
-#ifndef GS_LEAF_ILP
-#define GS_LEAF_ILP 1
-#endif
-                if constexpr ((FEAT & GS_FEAT_SPHLEAF) != 0 && GS_LEAF_ILP) {
+                if constexpr ((FEAT & GS_FEAT_SPHLEAF) != 0) {
                     // Sphere-only trees: a leaf run's second sphere (the next record, when it
                     // is a leaf) is read right away and both spheres' roots are computed as
                     // two independent chains; they are then accepted in order, the second
@@ -2373,12 +2084,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         next = next2;
                     }
                     closest32 = (float)closest;
-                    if constexpr (kSaluCount) {  // (uniform increments: one LDS add per wave each)
-                        atomicAdd(&s_cnt[C_SPH], 1ull);
-                        if (two) atomicAdd(&s_cnt[C_SPH], 1ull);
-                    } else {
-                        c_sph += 1u + (uint32_t)two;
-                    }
+                    c_sph += 1u + (uint32_t)two;
                     GS_MARK("sphere_end");
                 } else if ((FEAT & GS_FEAT_SPHLEAF) != 0 || (ref >> GS_REF_SHIFT) == GS_REF_SPHERE) {
 #ifdef GS_STAMPS
@@ -2399,12 +2105,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     // A leaf pass whose other-kind lanes all sit at one leaf (the Cornell box:
                     // always, with single node steps) tests it with scalar loads.
                     const uint32_t r0 = __builtin_amdgcn_readfirstlane(ref);
-#ifndef GS_UNI_MN
-#define GS_UNI_MN 1
-#endif
-                    // (GS_UNI_MN 0: media / nested-BVH kernels without the scalar-load copy)
-                    const bool uni = (GS_UNI_MN || !(FEAT & (GS_FEAT_MEDIA | GS_FEAT_NESTED))) &&
-                                     __builtin_amdgcn_ballot_w64(ref != r0) == 0;
+                    const bool uni = __builtin_amdgcn_ballot_w64(ref != r0) == 0;
                     LeafHit lh;
                     if (uni) lh = leaf_other<FEAT, true>(sc, qs, r0, ray, tmin, closest, rng, s_cnt);
                     else lh = leaf_other<FEAT, false>(sc, qs, ref, ray, tmin, closest, rng, s_cnt);
@@ -2427,7 +2128,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 // A template feature: trees without such pairs (the Cornell box's quads and
                 // instances) lose ~2% to the loop's mere presence (MI355X C3).
 #pragma unroll 1
-                for (int k = 1; (FEAT & GS_FEAT_LEAFRUN) && !((FEAT & GS_FEAT_SPHLEAF) != 0 && GS_LEAF_ILP) &&
+                for (int k = 1; (FEAT & GS_FEAT_LEAFRUN) && (FEAT & GS_FEAT_SPHLEAF) == 0 &&
                                 k < GS_LEAF_RUN && cur > THR_END; k++) {
                     load_tleaf<(FEAT & GS_FEAT_LDSTREE) != 0>(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr,
                                                          next, ref);
@@ -2448,10 +2149,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 }  // take_leaf
                 GS_MARK("leaf_end");
             }
-#ifndef GS_REMAT_RC
-#define GS_REMAT_RC 1
-#endif
-#if GS_REMAT_RC
             // Nested-BVH kernels and media kernels with sphere leaf runs: the certified test's
             // ray constants are recomputed after a leaf pass (the same function of the same
             // ray), so they are not live through leaf_other, whose medium and nested tests
@@ -2465,7 +2162,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     rc = make_cert(ray.o, inv);
                 }
             }
-#endif
 #ifdef GS_STAMPS
             {
                 uint64_t tp1;
@@ -2620,9 +2316,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #undef GS_TP
 
     // flush counters: LDS -> global, one atomic per counter per block
-    if constexpr (kSaluCount) {
-        if (lane == 0) atomicAdd(&s_cnt[C_NODES], (unsigned long long)w_nodes);
-    }
     atomicAdd(&s_cnt[C_NODES], (unsigned long long)c_nodes);
     atomicAdd(&s_cnt[C_SPH], (unsigned long long)c_sph);
     __syncthreads();
@@ -2864,12 +2557,15 @@ __global__ void gs_round_combine_kernel(const KParams* __restrict__ P, uint32_t 
 
 // =============================================================== host side
 static thread_local std::string tl_err;
-static int32_t g_shade_batch = 0;   // 0: the scene's own (52, or GS_KIND_SHADE_BATCH with BVHs under instances);  // swept on MI355X C4 (chunked, uniform loop): 48 -> 3502, 52 -> 3535-3568, 56 -> 3506-3536 Msamples/s
-static int32_t g_blocks_per_cu = 0;  // 0 = occupancy query
-static int32_t g_node_steps = 0;  // 0: the scene's own (gs_device_scene.node_steps)
+// Process-wide tuning (the gs_set_* / gs_debug_set_* setters).  Atomics: a setter may run
+// while another thread launches; each launch reads every value once, so
+// one launch never mixes two settings of the same knob.
+static std::atomic<int32_t> g_shade_batch{0};   // 0: the scene's own (52, or GS_KIND_SHADE_BATCH with BVHs under instances);  // swept on MI355X C4 (chunked, uniform loop): 48 -> 3502, 52 -> 3535-3568, 56 -> 3506-3536 Msamples/s
+static std::atomic<int32_t> g_blocks_per_cu{0};  // 0 = occupancy query
+static std::atomic<int32_t> g_node_steps{0};  // 0: the scene's own (gs_device_scene.node_steps)
 // leaf batch: 0 = the scene's choice (12: swept on MI355X C4 with leaf runs: 8 -> 4586, 10 ->
 // 4632, 12 -> 4648-4651, 14 -> 4624, 16 -> 4592; GS_KIND_LEAF_BATCH for kind-batched kernels)
-static int32_t g_leaf_batch = 0;
+static std::atomic<int32_t> g_leaf_batch{0};
 #ifndef GS_KIND_SHADE_BATCH
 #define GS_KIND_SHADE_BATCH 44
 #endif
@@ -2885,7 +2581,7 @@ static int32_t g_leaf_batch = 0;
 #ifndef GS_LDS_MIRROR
 #define GS_LDS_MIRROR -1
 #endif
-static int64_t g_lds_mirror = GS_LDS_MIRROR;
+static const int64_t g_lds_mirror = GS_LDS_MIRROR;  // (compile-time A/B only)
 static int64_t lds_mirror_budget() {
     const int64_t share = (int64_t)160 * 1024 * GS_BLOCK / (GS_MIN_WAVES * 4 * 64);  // the block's share of the CU
     // (sized for fixed-spp launches; an adaptive launch's larger lane state shrinks the
@@ -2897,17 +2593,17 @@ static int64_t lds_mirror_budget() {
 // C4 rank 0 / rank 3 of N (tools/rank_sim.py; ms): N=1: 4 -> 658.4, 8 -> 658.7,
 // 16 -> 648.3, 32 -> 647.3; N=8: 4 -> 89.6, 8 -> 89.6, 16 -> 89.7, 32 -> 95.8 (max of the
 // two ranks).  16 is within noise of the best at both ends.
-static int32_t g_sample_chunk = -1;
-static int32_t g_placement = 1;  // 1: placement pilot at a scene's first launch; 0: the static estimate only
-static uint64_t g_partial_budget = 4ull << 30;  // auto chunks: at most 4 GiB of chunk sums (per launch slot)
+static std::atomic<int32_t> g_sample_chunk{-1};
+static std::atomic<int32_t> g_placement{1};  // 1: placement pilot at a scene's first launch; 0: the static estimate only
+static std::atomic<uint64_t> g_partial_budget{4ull << 30};  // auto chunks: at most 4 GiB of chunk sums (per launch slot)
 // Adaptive settings (more than one batch): 1 = batch rounds (gs_round_*_kernel), 0 = the
 // per-lane loop (one work item per pixel running every batch).  Bit-identical results.
-static int32_t g_adaptive_rounds = 1;  // 1 auto (GS_ROUND_MIN_CAP), 2 always rounds, 0 never
+static std::atomic<int32_t> g_adaptive_rounds{1};  // 1 auto (GS_ROUND_MIN_CAP), 2 always rounds, 0 never
 // Work items of a round: 0 split (default; measured on MI355X, A2 cornell_box 1024^2: split
 // 7520, whole-batch items while the active pixels fill the lanes twice 5910 Msamples/s;
 // A1 hdri 19738 vs 18124), 1 whole-batch items, -1 whole while the active pixels fill the
 // lanes twice.
-static int32_t g_round_whole = 0;
+static std::atomic<int32_t> g_round_whole{0};
 // Auto mode: batch rounds when a pixel can take at least this many samples ((max_samples /
 // batch + 1) x batch): the per-lane loop's tail is up to that many samples in one lane.
 // MI355X: A2 cornell_box (cap 1024) rounds 7520 vs per-lane 5394 Msamples/s; A1 hdri (cap
@@ -3028,16 +2724,13 @@ struct Placed {
     std::vector<uint32_t> pos;  // tree record -> its position in tnodes / tleaves
     uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_nrecs = 0, lds_cubes = 0, root = THR_END;
 };
-#ifndef GS_LDS_LEAVES
-#define GS_LDS_LEAVES 1  // 0: mirror node records only
-#endif
 // Order the records by how likely a ray tests them and fill the block's LDS byte budget in
 // that order (32-B node records, 48-B leaf records; quads take the rest).  `visits` (one
 // count per record, nullable): measured by a pilot launch (GS_FEAT_VISITS), ranked by
 // visits per byte, which maximises the visits the mirror serves; the static estimate
 // orders the unvisited and serves when there is no pilot.  Records outside the mirror
 // stay in pre-order.
-// The aligned form of a quad's traversal record (quad_test, GS_AQUAD) when its normal is
+// The aligned form of a quad (cube_record) when its normal is
 // exactly +-e_a, w is zero off axis a, and u, v are each non-zero on one other axis.
 static bool aligned_tquad(const gs_quad& q, TQuad& out) {
     int ax = -1;
@@ -3078,7 +2771,7 @@ static bool aligned_tquad(const gs_quad& q, TQuad& out) {
     return true;
 }
 
-static int g_cube_lists = 1;  // gs_debug_set_cube_lists
+static std::atomic<int32_t> g_cube_lists{1};  // gs_debug_set_cube_lists
 // A Quad::cube list's device record (cube_test): six consecutive quads whose aligned forms
 // carry cube_code(k) in order and equal, field by field, what cube_src derives from the 12
 // numbers taken from them.  Returns false (the list keeps the loop) otherwise.
@@ -3136,7 +2829,6 @@ static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* 
     int64_t used = 0;
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t r = order[i];
-        if (!GS_LDS_LEAVES && t.leaf[r]) continue;
         const int64_t sz = rec_bytes(r);
         if (used + sz > budget) {
             if (used + (int64_t)sizeof(TNode) > budget) break;
@@ -3159,7 +2851,7 @@ static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* 
         if ((int64_t)q < fit) out.lds_quads = q + 1;
     used += (int64_t)out.lds_quads * (int64_t)sizeof(TQuad);
     // then the Quad::cube records (cube order)
-    out.lds_cubes = GS_CUBE_LDS ? (uint32_t)std::min<int64_t>(n_cubes, std::max<int64_t>(0, budget - used) / (GS_CUBE_DOUBLES * 8)) : 0u;
+    out.lds_cubes = (uint32_t)std::min<int64_t>(n_cubes, std::max<int64_t>(0, budget - used) / (GS_CUBE_DOUBLES * 8));
     // The mirrored records take their positions in rank order, so a launch that must
     // shrink the prefixes (a larger lane state, gs_render_tiles_timed_async) drops the
     // least-tested ones; the rest keep pre-order.
@@ -3244,9 +2936,10 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
         if (k == GS_REF_NODE || k == GS_REF_MEDIUM || k == GS_REF_INSTANCE) return 2;
         return prim_ok(cur) ? 0 : 1;
     };
-    // A BVH under an instance chain: nodes in range, leaves lists or primitives, depth
-    // within the device's private stack.  Subtrees may be shared between chains
-    // (instancing); the depth bound ends cycles and a visit budget ends blow-ups.
+    // A BVH under an instance chain: nodes in range, leaves lists or primitives, depth at
+    // most GS_NESTED_STACK (the device walk is threaded and needs no stack; the bound keeps
+    // the host's threading finite).  Subtrees may be shared between chains (instancing);
+    // the depth bound ends cycles and a visit budget ends blow-ups.
     bool nested = false;
     uint64_t nested_budget = 64ull << 20;
     auto nested_ok = [&](uint32_t root) -> int {
@@ -3384,20 +3077,6 @@ bool encode_rgbe(const float* c, uint32_t* out) {
     return false;
 }
 
-// The device ref of a HittableList whose members are consecutive quads (DREF_QRUN: every
-// Quad::cube), or the ref itself (final_scene's box tests read the list
-// record and then each member's ref before each quad, a chain of dependent global loads).
-uint32_t qrun_ref(const gs_flat_scene& s, uint32_t ref) {
-    if (!GS_QRUN || (ref >> GS_REF_SHIFT) != GS_REF_LIST || (ref & GS_REF_MASK) >= s.n_lists) return ref;
-    const gs_list& l = s.lists[ref & GS_REF_MASK];
-    if (l.count == 0 || l.count >= 64 || (uint64_t)l.first + l.count > s.n_list_refs) return ref;
-    const uint32_t q0 = s.list_refs[l.first];
-    if ((q0 >> GS_REF_SHIFT) != GS_REF_QUAD || (q0 & GS_REF_MASK) + l.count > QRUN_FIRST_MASK) return ref;
-    for (uint32_t k = 0; k < l.count; k++)
-        if (s.list_refs[l.first + k] != q0 + k) return ref;
-    return (DREF_QRUN << GS_REF_SHIFT) | (q0 & GS_REF_MASK) | (l.count << QRUN_COUNT_SHIFT);
-}
-
 // Does the texture tree under `t` contain an image (=> sphere uv must be computed)?
 bool tex_needs_uv(const gs_flat_scene& s, uint32_t t, int depth = 0) {
     if (t >= s.n_textures || depth > 16) return false;
@@ -3457,7 +3136,7 @@ gs_status gs_debug_set_cube_lists(int32_t on) {
 }
 
 gs_status gs_debug_set_partial_budget(uint64_t bytes) {
-    g_partial_budget = bytes ? bytes : (4ull << 30);
+    g_partial_budget.store(bytes ? bytes : (4ull << 30));
     return GS_OK;
 }
 
@@ -3481,22 +3160,17 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     {
         struct Cube {
             uint32_t list, q0;
-            double area;
             double rec[GS_CUBE_DOUBLES];
         };
         std::vector<Cube> found;
-        for (uint32_t i = 0; GS_CUBE && g_cube_lists && i < s->n_lists; i++) {
+        for (uint32_t i = 0; g_cube_lists && i < s->n_lists; i++) {
             Cube c;
             if (!cube_record(*s, s->lists[i], c.q0, c.rec)) continue;
             c.list = i;
-            const double dx = c.rec[6], dy = c.rec[7], dz = c.rec[8];
-            c.area = std::fabs(dx * dy) + std::fabs(dy * dz) + std::fabs(dx * dz);
             found.push_back(c);
         }
-        // The LDS mirror holds a prefix of the cube records: the largest boxes first (the
-        // ones rays meet most, by surface area; GS_CUBE_ORDER 0 keeps list order).
-        if (GS_CUBE_ORDER)
-            std::stable_sort(found.begin(), found.end(), [](const Cube& x, const Cube& y) { return x.area > y.area; });
+        // (the LDS mirror holds a prefix of the cube records in list order: largest boxes
+        // first measured neutral, profiles/r04/ab_cube_order.txt)
         for (const Cube& c : found) {
             dlists[c.list] = gs_list{(uint32_t)(cubes.size() / GS_CUBE_DOUBLES), GS_CUBE_FLAG | c.q0};
             cubes.insert(cubes.end(), c.rec, c.rec + GS_CUBE_DOUBLES);
@@ -3558,7 +3232,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                         if (n.right != GS_REF_NONE) work.push_back({n.right, false, w.depth + 1u});
                         work.push_back({n.left, false, w.depth + 1u});
                     } else {
-                        nodes.push_back(DNode{0, 0, 0, 0, 0, 0, idx + 1u, qrun_ref(*s, w.x), 1u, 0u});
+                        nodes.push_back(DNode{0, 0, 0, 0, 0, 0, idx + 1u, w.x, 1u, 0u});
                     }
                 }
                 const uint32_t end = (uint32_t)nodes.size();
@@ -3628,11 +3302,6 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             }
         }
         if (nodes.size() > GS_REF_MASK) return fail(GS_ERR_UNSUPPORTED, "more than 2^28 nested BVH records");
-        // the ends of instance chains that are lists of consecutive quads (Translate(RotateY(
-        // Quad::cube)): the Cornell boxes, main.rs:476-492)
-        // (not the chains of medium boundaries: medium_test reads plain lists, inst_reached 2)
-        for (size_t ii = 0; ii < insts.size(); ii++)
-            if (inst_reached[ii] == 1) insts[ii].child = qrun_ref(*s, insts[ii].child);
     }
     std::vector<gs_medium> media(s->media, s->media + s->n_media);
     // The threaded top-level tree (see THR_END): pre-order records of nodes and leaf
@@ -3678,7 +3347,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                     rec.mxx = q.radius;
                 }
                 rec.left = idx + 1u;  // next
-                rec.right = qrun_ref(*s, x);  // the primitive's ref (a quad run: DREF_QRUN)
+                rec.right = x;  // the primitive's ref
                 thr.push_back(rec);
                 thr_leaf.push_back(1);
             }
@@ -3777,11 +3446,6 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         const gs_quad& q = s->quads[i];
         tquads[i] = TQuad{q.normal[0], q.normal[1], q.normal[2], q.d, q.q[0], q.q[1], q.q[2], q.u[0],
                           q.u[1],      q.u[2],      q.v[0],      q.v[1], q.v[2], q.w[0], q.w[1], q.w[2]};
-        if (!(GS_AQUAD && aligned_tquad(q, tquads[i]))) {  // a full record whose first word would read as the aligned form's tag
-            uint64_t bits;
-            std::memcpy(&bits, &tquads[i].nx, 8);
-            if (((uint32_t)(bits >> 32) & ~7u) == GS_AQ_TAG) tquads[i].nx = std::nan("");  // (any NaN normal misses)
-        }
     }
     std::vector<DSphere> sph(s->n_spheres);
     std::vector<uint32_t> sph_mat(s->n_spheres);
@@ -3979,7 +3643,8 @@ gs_status gs_device_scene_info(const gs_device_scene* ds, gs_scene_info* out) {
     i.lds_leaves = ds->lds_leaves;
     i.lds_quads = ds->lds_quads;
     i.feat = ds->feat;
-    i.node_steps = std::max(1, std::min<int32_t>(unroll_steps(ds->feat), g_node_steps > 0 ? g_node_steps : ds->node_steps));
+    const int32_t t_steps = g_node_steps.load(std::memory_order_relaxed);
+    i.node_steps = std::max(1, std::min<int32_t>(unroll_steps(ds->feat), t_steps > 0 ? t_steps : ds->node_steps));
     i.cert_boxes = ds->cert_boxes ? 1 : 0;
     i.nodes_per_leaf = ds->nodes_per_leaf;
     i.other_leaf_frac = ds->other_leaf_frac;
@@ -4150,14 +3815,16 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     kp.order = part->d_tile_order;
     // Split pixels into sample chunks only when the settings run exactly one batch:
     // max_samples < batch_size makes the first stop test (camera.rs:158) always true.
+    const int32_t t_sample_chunk = g_sample_chunk.load(std::memory_order_relaxed);
+    const uint64_t t_partial_budget = g_partial_budget.load(std::memory_order_relaxed);
     uint32_t chunk = 0, cpp = 1, fine_px = (uint32_t)cap, fine_chunk = 1, fine_cpp = 1;
-    if (g_sample_chunk != 0 && ss->max_samples < ss->batch_size) {
+    if (t_sample_chunk != 0 && ss->max_samples < ss->batch_size) {
         const uint32_t bs = ss->batch_size;
-        uint32_t c = g_sample_chunk > 0 ? (uint32_t)g_sample_chunk : std::max<uint32_t>(16u, (bs + 63u) / 64u);
+        uint32_t c = t_sample_chunk > 0 ? (uint32_t)t_sample_chunk : std::max<uint32_t>(16u, (bs + 63u) / 64u);
         if ((bs + c - 1) / c > 64u) c = (bs + 63u) / 64u;  // at most 64 chunks per pixel
-        if (g_sample_chunk < 0)
-            while (c < bs && (uint64_t)cap * ((bs + c - 1) / c) * 24u > g_partial_budget) c *= 2u;
-        if (g_sample_chunk < 0) {
+        if (t_sample_chunk < 0)
+            while (c < bs && (uint64_t)cap * ((bs + c - 1) / c) * 24u > t_partial_budget) c *= 2u;
+        if (t_sample_chunk < 0) {
             // Guided tail: a work item of c samples started just before the queue runs dry
             // can keep its lane busy for c samples while every other lane idles, and a frame
             // with few items per lane ends on them (MI355X final_scene 400x400 x 64 spp,
@@ -4175,7 +3842,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
                 const uint64_t ft = std::min<uint64_t>(slots, (want + tile_px * bs - 1) / (tile_px * bs));
                 const uint32_t fpx = (uint32_t)((slots - ft) * tile_px), fcpp = (bs + fc - 1) / fc;
                 const uint64_t items = (uint64_t)fpx * ((bs + c - 1) / c) + ((uint64_t)cap - fpx) * fcpp;
-                if (items * 24u <= g_partial_budget && items < 0xFFFFFFFFull) {
+                if (items * 24u <= t_partial_budget && items < 0xFFFFFFFFull) {
                     fine_px = fpx;
                     fine_chunk = fc;
                     fine_cpp = fcpp;
@@ -4199,10 +3866,11 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
 #else
     const bool visit_out = outs->item_visits != nullptr;
 #endif
-    if (g_adaptive_rounds && g_sample_chunk != 0 && ss->max_samples >= ss->batch_size && !visit_out && !va) {
+    const int32_t t_adaptive = g_adaptive_rounds.load(std::memory_order_relaxed);
+    if (t_adaptive && t_sample_chunk != 0 && ss->max_samples >= ss->batch_size && !visit_out && !va) {
         const uint64_t R = (uint64_t)ss->max_samples / ss->batch_size + 1u;
-        const uint64_t sp = std::min<uint64_t>((uint64_t)cap, g_partial_budget / ((uint64_t)ss->batch_size * 24u));
-        const bool want = g_adaptive_rounds == 2 || R * ss->batch_size >= GS_ROUND_MIN_CAP;
+        const uint64_t sp = std::min<uint64_t>((uint64_t)cap, t_partial_budget / ((uint64_t)ss->batch_size * 24u));
+        const bool want = t_adaptive == 2 || R * ss->batch_size >= GS_ROUND_MIN_CAP;
         if (want && R <= kMaxRounds && sp >= 1 && sp * ss->batch_size < 0x7FFFFFFFull) {
             n_rounds = (uint32_t)R;
             seg_px = (uint32_t)sp;
@@ -4235,6 +3903,10 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     kp.item_visits = outs->item_visits;
     kp.visits = va ? va->visits : nullptr;
     kp.visit_leaf_base = va ? va->leaf_base : 0u;
+    // (under the scene's mutex from here: the placement pilot's end rewrites the records,
+    // the root and the mirror prefixes under it, pilot_end)
+    gs_device_scene* mds = const_cast<gs_device_scene*>(ds);
+    std::lock_guard<std::mutex> lock(mds->mu);
     KArgs a{};
     a.tnodes = ds->tnodes;
     a.tboxes = ds->tboxes;
@@ -4242,11 +3914,11 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     a.tquads = ds->tquads;
     a.root = ds->thr_root;
     a.cert_boxes = ds->cert_boxes ? 1 : 0;
-    a.shade_batch = g_shade_batch > 0 ? g_shade_batch : ds->shade_batch;
-    a.leaf_batch = std::max<int32_t>(1, g_leaf_batch > 0 ? g_leaf_batch : ds->leaf_batch);  // (0 would never step a node)
-    a.node_steps = std::max(1, std::min<int32_t>(unroll_steps(ds->feat), g_node_steps > 0 ? g_node_steps : ds->node_steps));
-    gs_device_scene* mds = const_cast<gs_device_scene*>(ds);
-    std::lock_guard<std::mutex> lock(mds->mu);
+    const int32_t t_shade = g_shade_batch.load(std::memory_order_relaxed), t_leaf = g_leaf_batch.load(std::memory_order_relaxed),
+                  t_steps = g_node_steps.load(std::memory_order_relaxed);
+    a.shade_batch = t_shade > 0 ? t_shade : ds->shade_batch;
+    a.leaf_batch = std::max<int32_t>(1, t_leaf > 0 ? t_leaf : ds->leaf_batch);  // (0 would never step a node)
+    a.node_steps = std::max(1, std::min<int32_t>(unroll_steps(ds->feat), t_steps > 0 ? t_steps : ds->node_steps));
     const bool chunked = kp.chunk != 0;
     gs_device_scene::LaunchCfg& lc = mds->lcfg[chunked ? 1 : 0];
     if (!lc.ready) {
@@ -4298,7 +3970,8 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     a.lds_cubes = lc.lds_cubes;
     a.cubes = ds->dev.cubes;
     a.lane_nd = lane_nd(chunked, ds->feat);
-    const int per_cu = g_blocks_per_cu > 0 ? g_blocks_per_cu : lc.per_cu;
+    const int32_t t_bpc = g_blocks_per_cu.load(std::memory_order_relaxed);
+    const int per_cu = t_bpc > 0 ? t_bpc : lc.per_cu;
     int64_t blocks = (int64_t)cus * per_cu;
     // no more waves than work: one lane per item at most (a round's items: at most one per sample)
     int64_t max_blocks = ((int64_t)(n_rounds ? (uint64_t)seg_px * ss->batch_size : kp.n_items) + GS_BLOCK - 1) / GS_BLOCK;
@@ -4397,8 +4070,8 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         const unsigned g_comb = (unsigned)std::min<int64_t>((seg_px + 255) / 256, 8192);
         for (uint32_t r = 0; r < n_rounds; r++)
             for (uint32_t sg = 0; sg < n_segs; sg++) {
-                hipLaunchKernelGGL(gs_round_params_kernel, dim3(1), dim3(64), 0, st, dP, r, sg, seg_px, g_sample_chunk,
-                                   g_round_whole);
+                hipLaunchKernelGGL(gs_round_params_kernel, dim3(1), dim3(64), 0, st, dP, r, sg, seg_px, t_sample_chunk,
+                                   g_round_whole.load(std::memory_order_relaxed));
                 hipLaunchKernelGGL(kernel_for(lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
                 hipLaunchKernelGGL(gs_round_combine_kernel, dim3(g_comb), dim3(256), 0, st, (const KParams*)dP, r);
             }
@@ -4410,12 +4083,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         return GS_OK;
     }
     if (k_begin) HIPCHK(hipEventRecord(k_begin, st));
-    // (per-pixel visit counts: the pilot's instantiation, which counts per lane, GS_SALU_COUNT)
-#if defined(GS_STAMPS) || defined(GS_CERT_CHECK)
     const bool pilot_kernel = va != nullptr;
-#else
-    const bool pilot_kernel = va != nullptr || (GS_SALU_COUNT && outs->item_visits != nullptr);
-#endif
     hipLaunchKernelGGL(kernel_for(pilot_kernel ? (GS_FEAT_PILOT | (lc.feat & GS_FEAT_NSPH)) : lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
     if (k_end) HIPCHK(hipEventRecord(k_end, st));
@@ -4508,14 +4176,22 @@ static gs_status pilot_end(gs_device_scene* ds, PilotRun& pr) {
     for (size_t i = 0; i < t.rec.size(); i++) counts[i] = t.leaf[i] ? vis[(size_t)nn + ds->pos[i]] : vis[ds->pos[i]];
     Placed pl = place_records(t, &counts, ds->single_quads, ds->mirror_budget, ds->n_nrecs, ds->n_cubes);
     if (pl.tnodes.size() != nn || pl.tleaves.size() != nl) return fail(GS_ERR_HIP, "placement changed the record counts");
-    // Nothing of this scene runs on the device yet (the pilot was its first launch and has
-    // finished), so the arrays are rewritten in place.
-    HIPCHK(hipMemcpy(const_cast<TNode*>(ds->tnodes), pl.tnodes.data(), pl.tnodes.size() * sizeof(TNode), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(const_cast<TBox*>(ds->tboxes), pl.tboxes.data(), pl.tboxes.size() * sizeof(TBox), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(const_cast<TLeaf*>(ds->tleaves), pl.tleaves.data(), pl.tleaves.size() * sizeof(TLeaf),
-                     hipMemcpyHostToDevice));
     {
+        // The arrays are rewritten in place, so nothing of this scene may be running: the
+        // pilot is not always the scene's first launch (pilot_due defers it past small ones,
+        // which may still be in flight on other streams).  Every launch records its slot's
+        // `done` event under `mu` before it returns, so with `mu` held every launch enqueued
+        // so far has an event to wait for, and none can start until the records and the
+        // launch shape below agree again.
         std::lock_guard<std::mutex> lock(ds->mu);
+        for (int k = 0; k < kLaunchSlots; k++)
+            if (ds->slots[k].used) HIPCHK(hipEventSynchronize(ds->slots[k].done));
+        HIPCHK(hipMemcpy(const_cast<TNode*>(ds->tnodes), pl.tnodes.data(), pl.tnodes.size() * sizeof(TNode),
+                         hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(const_cast<TBox*>(ds->tboxes), pl.tboxes.data(), pl.tboxes.size() * sizeof(TBox),
+                         hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(const_cast<TLeaf*>(ds->tleaves), pl.tleaves.data(), pl.tleaves.size() * sizeof(TLeaf),
+                         hipMemcpyHostToDevice));
         ds->thr_root = pl.root;
         ds->lds_nodes = pl.lds_nodes;
         ds->lds_leaves = pl.lds_leaves;

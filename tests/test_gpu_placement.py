@@ -104,3 +104,39 @@ def test_small_launches_leave_the_pilot_pending():
     torch.cuda.synchronize()
     assert r.scene_info()["placement"] == 2
     r.close()
+
+
+def test_pilot_waits_for_launches_in_flight():
+    """the pilot rewrites the scene's records in place, and it is not always the
+    scene's first launch (small launches leave it pending).  A small launch still queued on
+    stream A (behind a spin kernel) when a large launch on stream B runs the pilot must
+    render with the records it was launched with: pilot_end waits for every launch slot's
+    event before the rewrite.  Both frames equal those of a scene that never pilots."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    small = scenes.config("C4", width=160, spp=4)
+    big = scenes.config("C4", width=160, spp=32)
+
+    def frames(r, sa, sb, spin):
+        a = torch.zeros(r.capacity * 3, dtype=torch.float32, device=dev)
+        b = torch.zeros(r.capacity * 3, dtype=torch.float32, device=dev)
+        if spin:
+            with torch.cuda.stream(sa):
+                torch.cuda._sleep(200_000_000)  # ~0.1 s: the small launch waits behind it
+        r.render_async(a.data_ptr(), 0, sa.cuda_stream, seed=3)
+        N.check(N.lib.gs_render_tiles_async(r.dev, C.byref(r.cam), C.byref(big.settings), 5, C.byref(r.part),
+                                            C.c_void_p(b.data_ptr()), None, C.c_void_p(sb.cuda_stream)))
+        torch.cuda.synchronize()
+        return a.cpu().numpy(), b.cpu().numpy()
+
+    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    with _placement(0):
+        r0 = g.Renderer(small, 0, 1, 64)
+        ref_a, ref_b = frames(r0, sa, sb, False)
+        r0.close()
+    r = g.Renderer(small, 0, 1, 64)
+    got_a, got_b = frames(r, sa, sb, True)
+    assert r.scene_info()["placement"] == 2  # the large launch ran the pilot
+    r.close()
+    assert np.array_equal(got_a, ref_a)
+    assert np.array_equal(got_b, ref_b)

@@ -11,6 +11,7 @@ FETCH_SIZE / WRITE_SIZE are KB and FETCH_SIZE counts half the bytes of wide read
 hbm_bytes_per_launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
 """
 import argparse
+import re
 import csv
 import glob
 import json
@@ -23,8 +24,10 @@ def main():
     ap.add_argument("root")
     ap.add_argument("out")
     ap.add_argument("--kernel", default="gs_render_kernel")
-    ap.add_argument("--exclude", default="gs_render_kernel<55>",
-                    help="dispatches to skip (default: the placement pilot's instantiation, GS_FEAT_PILOT)")
+    ap.add_argument("--exclude", default="",
+                    help="comma-separated kernel-name substrings to skip as well (the placement pilot's "
+                         "counting instantiations -- template argument with GS_FEAT_VISITS, 32: <55>, <183> "
+                         "-- are always skipped)")
     ap.add_argument("--config", default="C4")
     ap.add_argument("--round", type=int, default=3)
     ap.add_argument("--lib", default=None, help="the library profiled (default: the in-tree libgrayshift.so)")
@@ -35,12 +38,21 @@ def main():
     lib = a.lib or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "grayshift_amd",
                                 "libgrayshift.so")
     h = code_object_hash(lib)
+    excl = [x for x in a.exclude.split(",") if x]
+
+    def skipped(name):
+        # the pilot's instantiations count every record's tests (GS_FEAT_VISITS = 32)
+        m = re.search(r"gs_render_kernel<(\d+)>", name)
+        if m and int(m.group(1)) & 32:
+            return True
+        return any(x in name for x in excl)
+
     vals = defaultdict(float)
     dispatches = defaultdict(set)
     dur = []
     for f in sorted(glob.glob(os.path.join(a.root, "pmc_*", "run_counter_collection.csv"))):
         for row in csv.DictReader(open(f)):
-            if a.kernel not in row["Kernel_Name"] or (a.exclude and a.exclude in row["Kernel_Name"]):
+            if a.kernel not in row["Kernel_Name"] or skipped(row["Kernel_Name"]):
                 continue
             name = row["Counter_Name"]
             vals[name] += float(row["Counter_Value"])
@@ -48,7 +60,7 @@ def main():
         kt = f.replace("run_counter_collection.csv", "run_kernel_trace.csv")
         if os.path.exists(kt):
             for row in csv.DictReader(open(kt)):
-                if a.kernel in row["Kernel_Name"] and not (a.exclude and a.exclude in row["Kernel_Name"]):
+                if a.kernel in row["Kernel_Name"] and not skipped(row["Kernel_Name"]):
                     dur.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6)
     if not vals:
         raise SystemExit("no %s rows under %s/pmc_*" % (a.kernel, a.root))
