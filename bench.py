@@ -107,6 +107,8 @@ def parse():
     ap.add_argument("--blocks-per-cu", type=int, default=None)
     ap.add_argument("--leaf-batch", type=int, default=None)
     ap.add_argument("--node-steps", type=int, default=0, help="node steps per node pass (0: the scene's choice)")
+    ap.add_argument("--camera-batch", type=int, default=0,
+                    help="lanes wanting a camera ray before a wave generates them (0: the scene's choice)")
     ap.add_argument("--sample-chunk", type=int, default=None, help="samples per work item (-1 auto, 0 whole pixel)")
     ap.add_argument("--adaptive-mode", type=int, default=1, choices=[0, 1, 2],
                     help="adaptive settings (gs_set_adaptive_mode): 1 auto (default), 2 batch rounds, 0 the per-lane loop")
@@ -144,6 +146,7 @@ def load_scene(a):
     g.set_tuning(a.shade_batch or 0, a.blocks_per_cu or 0, 0 if a.leaf_batch is None else a.leaf_batch,
                  -1 if a.sample_chunk is None else a.sample_chunk)
     g._native.check(g._native.lib.gs_set_node_steps(a.node_steps))
+    g._native.check(g._native.lib.gs_set_camera_batch(a.camera_batch))
     g._native.check(g._native.lib.gs_set_adaptive_mode(a.adaptive_mode))
     if a.config in scenes.CONFIGS:
         return scenes.config(a.config, width=a.width, spp=a.spp)

@@ -275,31 +275,26 @@ __device__ __forceinline__ bool sphere_accept(d3 c, double r, const Ray& ray, do
     return true;
 }
 
-// sphere_accept split in two (the same operations in the same order): the roots, which
-// do not depend on the ray interval, and the acceptance against it.  Lets a leaf pass
-// compute two spheres' roots as independent chains before accepting them in order.
-struct SphereRoots {
-    double t1, t2;  // (h - sqrt(disc)) / a, (h + sqrt(disc)) / a
-    bool real;      // disc >= 0
+// sphere_accept split at the discriminant: its first half (h, disc: no root, no
+// interval), and its second half for a real disc -- the same operations in the same order.
+// Lets a leaf pass run the square root and the divisions once for whichever of a lane's
+// spheres needs them (GS_FEAT_SPHLEAF leaf runs, render.hip).
+struct SphereDisc {
+    double h, disc;
 };
-__device__ __forceinline__ SphereRoots sphere_roots(d3 c, double r, const Ray& ray, double a) {
+__device__ __forceinline__ SphereDisc sphere_disc(d3 c, double r, const Ray& ray, double a) {
     d3 oc = sub(c, ray.o);
-    double h = dot(ray.d, oc);
+    SphereDisc s;
+    s.h = dot(ray.d, oc);
     double cc = len2(oc) - r * r;
-    double disc = h * h - a * cc;
-    SphereRoots s;
-    s.real = !(disc < 0.0);
-    double sq = sqrt(s.real ? disc : 0.0);
-    s.t1 = (h - sq) / a;
-    s.t2 = (h + sq) / a;
+    s.disc = s.h * s.h - a * cc;
     return s;
 }
-__device__ __forceinline__ bool sphere_take(const SphereRoots& s, double tmin, double tmax, double& t_out) {
-    t_out = tmax;
-    if (!s.real) return false;
-    double t = s.t1;
+__device__ __forceinline__ bool sphere_root_take(double h, double disc, double a, double tmin, double tmax, double& t_out) {
+    double sq = sqrt(disc);
+    double t = (h - sq) / a;
     if (!(tmin < t && t < tmax)) {
-        t = s.t2;
+        t = (h + sq) / a;
         if (!(tmin < t && t < tmax)) return false;
     }
     t_out = t;

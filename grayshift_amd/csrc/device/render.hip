@@ -240,6 +240,7 @@ struct KArgs {
     int32_t shade_batch;
     int32_t leaf_batch;  // >= 1: tracing lanes at a leaf before a wave runs a leaf pass
     int32_t node_steps;  // node steps per node pass, 1 .. GS_NODE_STEPS (per scene, see gs_set_node_steps)
+    int32_t cam_batch;   // >= 1: lanes waiting for a camera ray before a wave generates them (gs_set_camera_batch)
     int32_t cert_boxes;  // every node coordinate |x| <= 1e15: cert rays may take box_cert
     uint32_t lds_nodes;  // node records [0, lds_nodes) are mirrored in each block's LDS,
     uint32_t lds_leaves; // then leaf records [0, lds_leaves)
@@ -1290,7 +1291,7 @@ __device__ __forceinline__ void count_visit(uint32_t* counts, uint32_t idx) {
         const uint32_t v = __builtin_amdgcn_readlane(idx, lead);
         const uint64_t same = __builtin_amdgcn_ballot_w64(idx == v);
         if ((threadIdx.x & 63u) == lead) atomicAdd(&counts[v], (uint32_t)__popcll(same));
-        m &= ~same;
+        m &= ~(same | (1ull << lead));
     }
 }
 
@@ -1362,8 +1363,9 @@ __attribute__((amdgpu_num_vgpr(GS_NUM_VGPR)))
 #endif
 __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs A) {
     extern __shared__ __align__(16) uint8_t smem[];
-#ifdef GS_STAMPS
-#endif
+    // An empty batch round (adaptive settings: no active pixel left in this segment) has no
+    // item to hand out: return before the mirror copy.
+    if (A.P->rounds && A.P->n_items == 0) return;
 
     // The records a ray most likely tests (placed first by the host) are mirrored in LDS;
     // a lane whose node / leaf index is below lds_nodes / lds_leaves reads it from there
@@ -1612,6 +1614,30 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             ray.o = org;
             ray.d = sub(ps, org);
             ray.time = wy_f64(rng);
+#if defined(GS_DIAG_DUP) && (GS_DIAG_DUP & 4)
+            {  // cost probe: get_ray's draws and arithmetic twice, plus begin_ray's reciprocals
+                uint64_t g2 = stream_seed(P->seed, pix, LI(L_SAMPLE));
+                asm volatile("" : "+v"(g2));
+                double ox2 = wy_f64(g2) - 0.5, oy2 = wy_f64(g2) - 0.5;
+                d3 ps2 = add(add(ld3(cam.starting_pixel_pos), muls(ld3(cam.pixel_delta_u), (double)pi + ox2)),
+                             muls(ld3(cam.pixel_delta_v), (double)pj + oy2));
+                d3 org2 = ld3(cam.center);
+                if (cam.defocus_angle > 0.0) {
+                    double dx, dy;
+#pragma unroll 1
+                    for (;;) {
+                        dx = wy_f64(g2) * 2.0 + -1.0;
+                        dy = wy_f64(g2) * 2.0 + -1.0;
+                        if (dx * dx + dy * dy + 0.0 * 0.0 < 1.0) break;
+                    }
+                    org2 = add(add(ld3(cam.center), muls(ld3(cam.defocus_disk_u), dx)), muls(ld3(cam.defocus_disk_v), dy));
+                }
+                const d3 d2 = sub(ps2, org2);
+                const double tm2 = wy_f64(g2);
+                const d3 inv2 = mk(1.0 / d2.x, 1.0 / d2.y, 1.0 / d2.z);
+                asm volatile("" ::"v"(inv2.x), "v"(inv2.y), "v"(inv2.z), "v"(tm2), "v"(org2.x), "v"(org2.y), "v"(org2.z));
+            }
+#endif
             Tr = Tg = Tb = 1.0;
             LI(L_DEPTH) = cam.max_depth;
             if (cam.max_depth > 0) {
@@ -1812,10 +1838,20 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             need = __builtin_amdgcn_ballot_w64(st == S_NEED);
         }
         if constexpr (kOldSites) break;
-        if (st == S_CAM) {
-            GS_MARK("adv_begin");
-            advance();
-            GS_MARK("adv_end");
+        // Camera rays in batches (round 5): get_ray's draws, the defocus rejection loop and
+        // the stream seed cost a wave as much for a few lanes as for all 64, and after a
+        // shade pass only the lanes whose sample ended (~20 of 57 on C4) want one.  So a
+        // wave waits until `cam_batch` lanes want a camera ray -- those lanes sit idle, like
+        // finished lanes, meanwhile -- unless no lane has a ray to trace or the queue is
+        // done.  Each lane's samples and draws are unchanged; only when they start moves.
+        const uint64_t cam_m = __builtin_amdgcn_ballot_w64(st == S_CAM);
+        if (cam_m != 0 && ((uint32_t)__popcll(cam_m) >= (uint32_t)A.cam_batch || qdone ||
+                           __builtin_amdgcn_ballot_w64(st == S_TRACE) == 0)) {
+            if (st == S_CAM) {
+                GS_MARK("adv_begin");
+                advance();
+                GS_MARK("adv_end");
+            }
         }
         if (qdone || __builtin_amdgcn_ballot_w64(st == S_NEED) == 0) break;
         }
@@ -1915,7 +1951,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     const uint32_t me = cur;  // this record
                     if constexpr (FAST) {
                         // the certified decision picks the link at once; lanes f32 cannot
-                        // decide (rare) run the reference's f64 test out of line
+                        // decide (rare) run the reference's f64 test out of line.  (Taking the
+                        // link once after the join saves the copy of `cur` but puts the hit
+                        // mask in an SGPR pair: VOP3 compare and select, +2 issue cycles.)
                         float d, thr;
                         bool h = box_cert_dt(__uint_as_float(ra.x), __uint_as_float(ra.y), __uint_as_float(rb.x),
                                              __uint_as_float(ra.z), __uint_as_float(ra.w), __uint_as_float(rb.y), rc,
@@ -2056,8 +2094,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 };
                 if constexpr ((FEAT & GS_FEAT_SPHLEAF) != 0) {
                     // Sphere-only trees: a leaf run's second sphere (the next record, when it
-                    // is a leaf) is read right away and both spheres' roots are computed as
-                    // two independent chains; they are then accepted in order, the second
+                    // is a leaf) is read right away and both discriminants are computed as two
+                    // independent chains; the roots are then taken in order, the second sphere
                     // against the interval the first left (sphere.rs:64-89, BVH.rs:73-80).
                     const bool two = cur_next_is_leaf(next);
                     double s2x, s2y, s2z, s2r;
@@ -2065,21 +2103,35 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     load_tleaf<(FEAT & GS_FEAT_LDSTREE) != 0>(s_leaves, A.tleaves, two ? next & ~THR_LEAF : cur & ~THR_LEAF,
                                                              A.lds_leaves, s2x, s2y, s2z, s2r, next2, ref2);
                     const double a = len2(ray.d);
-                    const SphereRoots q1 = sphere_roots(mk(scx, scy, scz), sr, ray, a);
-                    const SphereRoots q2 = sphere_roots(mk(s2x, s2y, s2z), s2r, ray, a);
+                    // Root rounds (round 5): the square root and the divisions run once for
+                    // the lane's first sphere with a real discriminant (sphere 1, else sphere 2),
+                    // then once more only for lanes where both were real.  Run per sphere, both
+                    // root blocks executed in most passes (C4 traces: 86% and 76% of leaf passes;
+                    // in rounds 97% and 19%).  MI355X C4: 8 025 -> 8 226 Msamples/s.  Order: a
+                    // lane whose sphere 1 is real takes it against `closest`, then sphere 2
+                    // against what it left; a lane whose sphere 1 is not real takes sphere 2
+                    // first, as the reference, whose sphere-1 test changed nothing.
+                    const SphereDisc q1 = sphere_disc(mk(scx, scy, scz), sr, ray, a);
+                    const SphereDisc q2 = sphere_disc(mk(s2x, s2y, s2z), s2r, ray, a);
+                    const bool real1 = !(q1.disc < 0.0), real2 = two && !(q2.disc < 0.0);
                     GS_MARK("sphere_begin");
                     double t;
-                    if (sphere_take(q1, tmin, closest, t)) {
-                        closest = t;
-                        hit_ref = ref;
+                    if (real1 || real2) {
+                        const double hA = real1 ? q1.h : q2.h, dA = real1 ? q1.disc : q2.disc;
+                        if (sphere_root_take(hA, dA, a, tmin, closest, t)) {
+                            closest = t;
+                            hit_ref = real1 ? ref : ref2;
+                        }
+                    }
+                    if (real1 && real2) {
+                        if (sphere_root_take(q2.h, q2.disc, a, tmin, closest, t)) {
+                            closest = t;
+                            hit_ref = ref2;
+                        }
                     }
                     if (two) {
                         if constexpr ((FEAT & GS_FEAT_VISITS) != 0) {
                             if (P->visits) count_visit(P->visits, P->visit_leaf_base + (next & ~THR_LEAF));
-                        }
-                        if (sphere_take(q2, tmin, closest, t)) {
-                            closest = t;
-                            hit_ref = ref2;
                         }
                         next = next2;
                     }
@@ -2190,6 +2242,17 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             if constexpr ((FEAT & (GS_FEAT_MIXED | GS_FEAT_MEDIA | GS_FEAT_NESTED)) != 0) {
                 GS_STAMP(r0);
                 GS_MARK("shade_begin");
+#if defined(GS_DIAG_DUP) && (GS_DIAG_DUP & 1)
+                {  // cost probe: the shade work twice (the copy's results consumed, its counts double)
+                    Ray r2 = ray;
+                    uint64_t g2 = rng;
+                    double c2 = closest;
+                    asm volatile("" : "+v"(r2.d.x), "+v"(c2));
+                    const ShadeOut s2 = shade(sc, r2, c2, hit_ref, LI(L_HINST), g2, s_cnt);
+                    asm volatile("" ::"v"(s2.col.x), "v"(s2.col.y), "v"(s2.col.z), "v"(s2.dir.x), "v"(s2.dir.y), "v"(s2.dir.z),
+                                 "v"(r2.o.x), "v"(g2), "v"(s2.cont));
+                }
+#endif
                 const ShadeOut s = shade(sc, ray, closest, hit_ref, LI(L_HINST), rng, s_cnt);
                 GS_MARK("shade_end");
                 GS_REGION(2, r0);
@@ -2566,6 +2629,7 @@ static std::atomic<int32_t> g_node_steps{0};  // 0: the scene's own (gs_device_s
 // leaf batch: 0 = the scene's choice (12: swept on MI355X C4 with leaf runs: 8 -> 4586, 10 ->
 // 4632, 12 -> 4648-4651, 14 -> 4624, 16 -> 4592; GS_KIND_LEAF_BATCH for kind-batched kernels)
 static std::atomic<int32_t> g_leaf_batch{0};
+static std::atomic<int32_t> g_cam_batch{0};  // 0: the scene's own (gs_set_camera_batch)
 #ifndef GS_KIND_SHADE_BATCH
 #define GS_KIND_SHADE_BATCH 44
 #endif
@@ -2674,6 +2738,7 @@ struct gs_device_scene {
     int32_t node_steps = GS_NODE_STEPS;      // node steps per node pass (from the tree's shape)
     int32_t leaf_batch = 12;                 // lanes at a leaf before a leaf pass (scene's choice)
     int32_t shade_batch = 52;                // finished lanes a wave shades together (scene's choice)
+    int32_t cam_batch = 1;                   // lanes waiting for camera rays before a wave runs get_ray
     uint32_t node_records = 0, leaf_records = 0;
     double nodes_per_leaf = 0.0, other_leaf_frac = 0.0;
     // Launch state, mutated by launches of a const scene: guarded by `mu`.
@@ -3096,6 +3161,12 @@ int32_t gs_version(void) { return GS_ABI_VERSION; }
 gs_status gs_set_node_steps(int32_t node_steps) {
     if (node_steps < 0 || node_steps > GS_NODE_STEPS) return fail(GS_ERR_ARG, "node_steps outside [0, GS_NODE_STEPS]");
     g_node_steps = node_steps;
+    return GS_OK;
+}
+
+gs_status gs_set_camera_batch(int32_t cam_batch) {
+    if (cam_batch < 0 || cam_batch > 64) return fail(GS_ERR_ARG, "camera batch outside [0, 64]");
+    g_cam_batch = cam_batch;
     return GS_OK;
 }
 
@@ -3919,6 +3990,8 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     a.shade_batch = t_shade > 0 ? t_shade : ds->shade_batch;
     a.leaf_batch = std::max<int32_t>(1, t_leaf > 0 ? t_leaf : ds->leaf_batch);  // (0 would never step a node)
     a.node_steps = std::max(1, std::min<int32_t>(unroll_steps(ds->feat), t_steps > 0 ? t_steps : ds->node_steps));
+    const int32_t t_cam = g_cam_batch.load(std::memory_order_relaxed);
+    a.cam_batch = std::max<int32_t>(1, t_cam > 0 ? t_cam : ds->cam_batch);
     const bool chunked = kp.chunk != 0;
     gs_device_scene::LaunchCfg& lc = mds->lcfg[chunked ? 1 : 0];
     if (!lc.ready) {

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 8
+#define GS_ABI_VERSION 9
 
 typedef int32_t gs_status;
 enum {
@@ -231,6 +231,14 @@ gs_status gs_set_tuning(int32_t shade_batch, int32_t blocks_per_cu, int32_t leaf
  * up to this many BVH node steps before the wave re-checks which lanes sit at leaves.
  * 0 (default) = the scene's own choice, from its tree's shape at gs_device_scene_create. */
 gs_status gs_set_node_steps(int32_t node_steps);
+
+/* Camera-ray batch, process-wide (ABI 9): lanes of a wave that want a camera ray (a new
+ * sample's Camera::get_ray, camera.rs:204-221) before the wave generates them together,
+ * in [0, 64]; 0 (default) = the scene's own choice.  Waiting lanes idle like finished
+ * ones; a wave never waits when none of its lanes has a ray to trace or the work queue
+ * is empty.  Every sample's draws and ray are unchanged: only when a lane starts its next
+ * sample moves, so frames and counters do not depend on it. */
+gs_status gs_set_camera_batch(int32_t cam_batch);
 
 /* Placement of the threaded BVH records (ABI 7).  1 (default): before a scene's first
  * launch, when its records do not all fit the per-block LDS mirror, a pilot renders the

@@ -16,7 +16,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KNOBS = ["shade_batch", "leaf_batch", "sample_chunk", "blocks_per_cu", "tile", "node_steps"]
+KNOBS = ["shade_batch", "leaf_batch", "sample_chunk", "blocks_per_cu", "tile", "node_steps", "camera_batch"]
 
 
 def main():
