@@ -1,7 +1,13 @@
 #!/usr/bin/env python3
 """Phase split of the megakernel (diagnostic build variants/stamps.so, -DGS_STAMPS).
-GS_LIB=grayshift_amd/variants/stamps.so python tools/stamps.py [--config C4] [tuning]"""
-import argparse, ctypes as C, os, sys
+GS_LIB=grayshift_amd/variants/stamps.so python tools/stamps.py [--config C4] [tuning] [--json DIR]
+
+--json DIR writes the lane-efficiency summary bench.py reads into its roofline
+(DIR/<config>_<product code-object hash>.json): each phase's wave clock and active lanes
+of 64, and lane_frac, their clock-weighted mean.  The stamps build is a
+different binary than the product (its clock reads perturb scheduling, so only shares are
+meaningful); the summary is keyed by the product library built from the same sources."""
+import argparse, ctypes as C, json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -15,6 +21,9 @@ def main():
     ap.add_argument("--leaf-batch", type=int, default=0, help="0: the scene's choice")
     ap.add_argument("--sample-chunk", type=int, default=-1)
     ap.add_argument("--node-steps", type=int, default=0, help="0: the scene's own")
+    ap.add_argument("--json", default=None, help="write the lane-efficiency summary into this directory")
+    ap.add_argument("--tag", default=None, help="the summary's config name (default: --config, or "
+                                                   "<config>_w<width>_s<spp> for an overridden size)")
     a = ap.parse_args()
     import torch
     import grayshift_amd as g
@@ -25,7 +34,7 @@ def main():
     r = g.Renderer(sc, 0, 1, 64)
     dev = torch.device("cuda", 0)
     packed = torch.zeros(r.capacity * 3, dtype=torch.float32, device=dev)
-    dbg = torch.zeros(max(32, r.capacity // 2 + 2), dtype=torch.int64, device=dev)
+    dbg = torch.zeros(max(40, r.capacity // 2 + 2), dtype=torch.int64, device=dev)
     N.check(N.lib.gs_render_tiles_debug_async(r.dev, C.byref(r.cam), C.byref(r.settings), 1, C.byref(r.part),
                                               C.c_void_p(packed.data_ptr()), None, C.c_void_p(dbg.data_ptr()), None))
     torch.cuda.synchronize()
@@ -61,6 +70,33 @@ def main():
         "%s %.1f%%" % (n, 100.0 * x / max(1, v[2])) for n, x in
         zip(["background", "reconstruct", "scatter (staged: all shading)", "-", "add_sample + chunk end"], reg)))
     # camera rays (advance) and begin_ray run at the loop head since r02: inside "refill"
+    it_adv, ln_adv = dbg[32:34].cpu().tolist()
+    phases = {  # wave clock, mean active lanes of 64
+        "node passes (per node step)": (node_clk, wlanes / max(1, wsteps)),
+        "leaf passes": (leaf_clk, ln_leaf / max(1, it_leaf)),
+        "shade passes": (v[2], ln_shade / max(1, it_shade)),
+    }
+    if it_adv:  # (kernels with BVHs under instances run get_ray per lane in the refill: not counted)
+        phases["refill + camera rays (per get_ray)"] = (v[0], ln_adv / it_adv)
+    tot_clk = sum(p[0] for p in phases.values())
+    lane_frac = sum(p[0] * p[1] / 64.0 for p in phases.values()) / max(1, tot_clk)
+    print("lanes of 64 by phase: " + "  ".join("%s %.1f" % (k, p[1]) for k, p in phases.items()) +
+          "  -> clock-weighted lane_frac %.3f" % lane_frac)
+    if a.json:
+        from grayshift_amd.codeobj import code_object_hash
+        prod = os.path.join(ROOT, "grayshift_amd", "libgrayshift.so")
+        h = code_object_hash(prod)
+        tag = a.tag or (a.config if a.width is None and a.spp is None else "%s_w%s_s%s" % (a.config, a.width, a.spp))
+        os.makedirs(a.json, exist_ok=True)
+        out = {"config": tag, "code_object": h, "stamps_library": os.environ.get("GS_LIB", ""),
+               "source": "tools/stamps.py on MI355X: the -DGS_STAMPS build's per-wave phase clocks and active-lane counts, one frame",
+               "phases": {k: {"wave_clock": int(p[0]), "active_lanes": round(p[1], 2)} for k, p in phases.items()},
+               "wave_clock_split": {"refill": v[0], "traverse": v[1], "shade": v[2]},
+               "lane_frac": round(lane_frac, 4),
+               "definition": "sum over phases of wave_clock x active_lanes / 64, over the phases' wave clock"}
+        path = os.path.join(a.json, "%s_%s.json" % (tag, h))
+        json.dump(out, open(path, "w"), indent=1)
+        print("wrote", path)
 
 
 if __name__ == "__main__":
