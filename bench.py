@@ -410,6 +410,19 @@ def roofline(a, c, world, kernel_ms, invalid):
     # (an overridden size has its own summary: <config>_w<width>_s<spp>_<hash>.json, e.g.
     # final_scene at 1440^2 x 64 spp from tools/gpu_final.sh)
     key = a.config if not invalid else "%s_w%s_s%s" % (a.config, a.width, a.spp)
+    # Lane efficiency: of the SIMD issue time `frac` counts, the share of
+    # the 64 lanes that did work -- the stamps build's active lanes per phase, weighted by each
+    # phase's wave clock (tools/stamps.py --json, profiles/stamps/<config>_<hash>.json); no
+    # gfx950 counter counts active lanes per VALU instruction.  useful_frac = frac x lane_frac.
+    spath = os.path.join(os.path.dirname(a.pmc_dir), "stamps", "%s_%s.json" % (key, h))
+    lane = None
+    if os.path.exists(spath):
+        sj = json.load(open(spath))
+        lane = sj["lane_frac"]
+        out.update({"lane_frac": lane, "lane_frac_by_phase": {k: v["active_lanes"] for k, v in sj["phases"].items()},
+                    "stamps": os.path.relpath(spath, ROOT)})
+    else:
+        out.update({"lane_frac": None, "stamps": "none for this code object (%s)" % os.path.relpath(spath, ROOT)})
     path = os.path.join(a.pmc_dir, "%s_%s.json" % (key, h))
     if not os.path.exists(path):
         out["pmc"] = "none for this code object (%s)" % os.path.relpath(path, ROOT)
@@ -446,6 +459,8 @@ def roofline(a, c, world, kernel_ms, invalid):
                 "wave_cycles_issue_stalled": round(float(k.get("SQ_WAIT_INST_ANY", 0.0)) / wc, 4),
                 "wave_cycles_issuing": round(float(k.get("SQ_ACTIVE_INST_ANY", 0.0)) / wc, 4),
                 "pmc": os.path.relpath(path, ROOT)})
+    if lane is not None:
+        out["useful_frac"] = round(out["frac"] * lane, 4)
     return out
 
 

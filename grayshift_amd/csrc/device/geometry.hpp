@@ -178,7 +178,9 @@ struct alignas(16) TNode {  // 32 B record of the threaded tree: f32 box (paired
     uint32_t hit, miss;
 };
 struct alignas(16) TLeaf {  // 48 B leaf record: a stationary sphere inline, next link, ABI ref
-    double cx, cy, cz, r;
+    // rr = radius * radius, Sphere::hit's `self.radius * self.radius` (sphere.rs:70) taken
+    // once on the host: the same IEEE product the test would take per ray (round 5)
+    double cx, cy, cz, rr;
     uint32_t next, ref, pad0, pad1;
 };
 struct alignas(16) TBox {  // 48 B: the node's f64 box (AABB.rs), for undecided and non-cert rays
@@ -257,11 +259,12 @@ __device__ __forceinline__ DNode box64(const TBox& b) {
 
 // Sphere::hit acceptance (sphere.rs:64-88): whether a root lies in the open interval,
 // and that root (t_out is written on every path, so callers carry no undefined value).
-__device__ __forceinline__ bool sphere_accept(d3 c, double r, const Ray& ray, double a, double tmin, double tmax,
-                                         double& t_out) {
+// (rr: the radius squared, r * r; leaf records carry it, TLeaf)
+__device__ __forceinline__ bool sphere_accept_rr(d3 c, double rr, const Ray& ray, double a, double tmin, double tmax,
+                                            double& t_out) {
     d3 oc = sub(c, ray.o);
     double h = dot(ray.d, oc);
-    double cc = len2(oc) - r * r;
+    double cc = len2(oc) - rr;
     double disc = h * h - a * cc;
     t_out = tmax;
     if (disc < 0.0) return false;
@@ -274,6 +277,10 @@ __device__ __forceinline__ bool sphere_accept(d3 c, double r, const Ray& ray, do
     t_out = t;
     return true;
 }
+__device__ __forceinline__ bool sphere_accept(d3 c, double r, const Ray& ray, double a, double tmin, double tmax,
+                                         double& t_out) {
+    return sphere_accept_rr(c, r * r, ray, a, tmin, tmax, t_out);
+}
 
 // sphere_accept split at the discriminant: its first half (h, disc: no root, no
 // interval), and its second half for a real disc -- the same operations in the same order.
@@ -282,11 +289,11 @@ __device__ __forceinline__ bool sphere_accept(d3 c, double r, const Ray& ray, do
 struct SphereDisc {
     double h, disc;
 };
-__device__ __forceinline__ SphereDisc sphere_disc(d3 c, double r, const Ray& ray, double a) {
+__device__ __forceinline__ SphereDisc sphere_disc_rr(d3 c, double rr, const Ray& ray, double a) {
     d3 oc = sub(c, ray.o);
     SphereDisc s;
     s.h = dot(ray.d, oc);
-    double cc = len2(oc) - r * r;
+    double cc = len2(oc) - rr;
     s.disc = s.h * s.h - a * cc;
     return s;
 }

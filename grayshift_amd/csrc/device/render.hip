@@ -67,9 +67,6 @@ using namespace gsd;
 #endif
 // The nested trees' records (BVHs under instances) mirrored in LDS after the quads, placed
 // shallowest first (0: read from global memory only)
-#ifndef GS_NESTED_LDS
-#define GS_NESTED_LDS 1
-#endif
 #define GS_NESTED_STACK 32  // max depth of a BVH under a Translate/RotateY chain (a validation bound; the walk is stackless)
 // Kernel feature flags (template argument): scenes without them compile the code out.
 #define GS_FEAT_MEDIA 1   // ConstantMedium leaves (RNG draws inside traversal)
@@ -84,24 +81,10 @@ using namespace gsd;
 #define GS_FEAT_VISITS 32 // count tests per threaded record (the placement pilot, run_pilot)
 #define GS_FEAT_SPHLEAF 64 // every top-level leaf is a stationary sphere (no media / nested BVHs):
                            // leaf passes without the other kinds' code or the kind test
-#ifndef GS_NSPH
-#define GS_NSPH 1
-#endif
-#define GS_FEAT_NSPH 128   // with GS_FEAT_NESTED: every nested leaf is a stationary sphere
-                           // (nested_leaf without the kind dispatch)
 #ifndef GS_NODE_STEPS
 #define GS_NODE_STEPS 8  // node steps per unrolled node pass (the render kernel, below)
 #endif
-// Kernels for scenes with nested sphere trees (GS_FEAT_NSPH: final_scene) may unroll a
-// different count (their node passes carry few lanes, 16.7 of 64): 16 measured final_scene
-// 2 469-2 521 against 8's 2 439-2 528 over four runs each -- within the spread, so 8; C4 with
-// 16 unrolled for every kernel: -0.4%, with 12: -1.3% (profiles/r04/ab_node_steps_unroll.txt).
-#ifndef GS_NSPH_NODE_STEPS
-#define GS_NSPH_NODE_STEPS 8  // 16: neutral within run-to-run spread (mean of four runs +1.2%)
-#endif
-__host__ __device__ constexpr int unroll_steps(int feat) {
-    return (feat & GS_FEAT_NSPH) != 0 ? GS_NSPH_NODE_STEPS : GS_NODE_STEPS;
-}
+__host__ __device__ constexpr int unroll_steps(int feat) { return GS_NODE_STEPS; }
 // The pilot's instantiation: every code path (any scene), plus the counts.
 #define GS_FEAT_PILOT (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_VISITS)
 
@@ -145,10 +128,10 @@ enum { C_RAYS = 0, C_NODES, C_SPH, C_MSPH, C_QUAD, C_TRI, C_INST, C_LIST, C_HITS
 #endif
 
 struct DevScene {
-    const DNode* nodes;   // nested trees' records with their f64 boxes (the f64 test)
-    const TNode* nrecs;   // the same records for the certified f32 test (nested_bvh)
-    uint32_t nested_cert; // every nested node coordinate |x| <= 1e15 (box_cert applies)
-    const double* nradii; // GS_FEAT_NSPH: the nested spheres' distinct radii (<= 16; nested_leaf)
+    // BVHs under Translate/RotateY chains (GS_FEAT_NESTED): their records are threaded into
+    // the node and leaf arrays with the top-level tree's; nroots[k] is the link of tree k's
+    // root record (an instance whose chain ends in tree k has the child GS_REF_NODE | k).
+    const uint32_t* nroots;
     const DSphere* spheres;
     const uint32_t* sphere_mat;
     const gs_msphere* mspheres;
@@ -227,6 +210,9 @@ struct KParams {
     uint32_t* active_buf[2];   // the two lists (rounds alternate)
     uint32_t* round_counts;    // [rounds + 1]: active pixels per round
     double* pstate;            // per packed pixel: the running Σr, Σg, Σb, Σlum, Σlum² (camera.rs:131-146)
+    // GS_FEAT_NESTED: per lane (block * GS_BLOCK + thread), the top-level ray while the lane
+    // walks a BVH under an instance chain: o, d (6 doubles), then the return link (u32)
+    double* nest_save;
 };
 
 // Hot kernel arguments: what the traversal loop reads every step.
@@ -245,8 +231,6 @@ struct KArgs {
     uint32_t lds_nodes;  // node records [0, lds_nodes) are mirrored in each block's LDS,
     uint32_t lds_leaves; // then leaf records [0, lds_leaves)
     uint32_t lds_quads;  // then quad records [0, lds_quads)
-    uint32_t lds_nrecs;  // then the nested trees' records [0, lds_nrecs) (GS_NESTED_LDS)
-    const TNode* nrecs;  // (the mirror's source)
     uint32_t lds_cubes;  // then the Quad::cube records [0, lds_cubes) (cube_test)
     const double* cubes; // (the mirror's source)
     uint32_t lane_nd;    // f64 lane-state fields in LDS: lane_nd(chunked)
@@ -280,6 +264,10 @@ __host__ __device__ inline uint32_t device_ref(uint32_t abi_ref) {
 // tagged with THR_LEAF; THR_END ends the walk.
 #define THR_END 0x7FFFFFFFu
 #define THR_LEAF 0x80000000u
+// The last links of a BVH under an instance chain (GS_FEAT_NESTED): "back to the top-level
+// ray" -- a leaf-tagged value no leaf index reaches (< 2^26), so a lane there waits for a
+// leaf pass like a lane at a leaf.
+#define THR_RET 0xFFFFFFFFu
 
 // Node and leaf records live in two arrays (32-B TNode, 48-B TLeaf: geometry.hpp); a link
 // is a node's byte offset (index << 5: the address arithmetic of a node step is then
@@ -337,10 +325,10 @@ __device__ __forceinline__ d3 inv_of(d3 d) {
     asm volatile("" : "+v"(d.x), "+v"(d.y), "+v"(d.z));
     return mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
 }
-// A leaf record: the sphere's centre and radius, its next link and its ABI ref.
+// A leaf record: the sphere's centre and radius squared, its next link and its ABI ref.
 template <bool LDS_ONLY>
 __device__ __forceinline__ void load_tleaf(const uint8_t* s_leaves, const TLeaf* g, uint32_t i, uint32_t lds_l,
-                                           double& cx, double& cy, double& cz, double& r, uint32_t& next,
+                                           double& cx, double& cy, double& cz, double& rr, uint32_t& next,
                                            uint32_t& ref) {
     u32x4 a, b;
     u32x2 d;
@@ -364,7 +352,7 @@ __device__ __forceinline__ void load_tleaf(const uint8_t* s_leaves, const TLeaf*
     cx = lo_hi(a.x, a.y);
     cy = lo_hi(a.z, a.w);
     cz = lo_hi(b.x, b.y);
-    r = lo_hi(b.z, b.w);
+    rr = lo_hi(b.z, b.w);
     next = d.x;
     ref = d.y;
 }
@@ -375,9 +363,6 @@ struct QuadSrc {
     const uint8_t* lds;
     const TQuad* g;
     uint32_t n_lds;
-    // the nested trees' records mirrored in LDS: [0, n_nlds) at nlds (GS_NESTED_LDS)
-    const uint8_t* nlds;
-    uint32_t n_nlds;
     // the Quad::cube records mirrored in LDS: [0, n_lcubes) at lcubes (cube_test)
     const uint8_t* lcubes;
     uint32_t n_lcubes;
@@ -431,22 +416,6 @@ __device__ __forceinline__ gs_medium ld_medium(const gs_medium* p) {
     v.density_neg_inv = q->density_neg_inv;
     return v;
 }
-__device__ __forceinline__ DNode ld_node_g(const DNode* p) {  // a nested-BVH node (global loads)
-    const auto q = sp<false>(reinterpret_cast<const u32x4*>(p));
-    const u32x4 a = q[0], b = q[1], c = q[2], d = q[3];
-    DNode n;
-    n.mnx = lo_hi(a.x, a.y);
-    n.mny = lo_hi(a.z, a.w);
-    n.mnz = lo_hi(b.x, b.y);
-    n.mxx = lo_hi(b.z, b.w);
-    n.mxy = lo_hi(c.x, c.y);
-    n.mxz = lo_hi(c.z, c.w);
-    n.left = d.x;
-    n.right = d.y;
-    n.pad0 = d.z;
-    n.pad1 = d.w;
-    return n;
-}
 template <bool UNI>
 __device__ __forceinline__ u32x4 quad_part(const QuadSrc& qs, uint32_t i, uint32_t k) {
     if (!UNI && i < qs.n_lds) return *(lds_u32x4*)(qs.lds + i * (uint32_t)sizeof(TQuad) + (k << 4));
@@ -488,6 +457,7 @@ struct LeafHit {
     bool hit;
     double t;
     uint32_t ref, inst;
+    uint32_t enter;  // GS_FEAT_NESTED: the chain ended in BVH tree `enter - 1` (0: it did not)
 };
 
 // One primitive ref against `ray` (already in the primitive's space); accepts into
@@ -664,7 +634,7 @@ __device__ __forceinline__ void shape_test(const DevScene& sc, const QuadSrc& qs
 // ConstantMedium::hit (volume.rs:32-63): the boundary hit over Interval::UNIVERSE, again
 // from t1 + 0.0001, both clipped to ray_t; then the free-flight distance from the lane's
 // RNG stream, drawn here, inside traversal, in the reference's visit order (:48).
-template <bool UNI, bool REUSE>
+template <bool UNI>
 __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& qs, uint32_t cur, const Ray& r, double tmin,
                                             double closest, uint32_t inst_ref, uint64_t& rng, LeafHit& res,
                                             unsigned long long* cnt) {
@@ -675,15 +645,13 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
         uint32_t boundary;
     } md{ld_u32<UNI>(&mp->boundary)};
     const double DMAX = 1.7976931348623157e308;  // f64::MAX; f64::MIN = -f64::MAX
-    // REUSE: |ray.d| now (the same value volume.rs:55 computes at the end), so the ray itself
-    // is not live through the boundary tests: they need only its transform into the
+    // |ray.d| now (the same value volume.rs:55 computes at the end), so the ray itself is
+    // not live through the boundary tests: they need only its transform into the
     // boundary's space, which the second boundary.hit call (volume.rs:38-41) would recompute
     // from the same ray bit for bit -- it is reused, and the second walk's instance tests
-    // are counted.  (Media-only kernels: without it they spill 12-20 B/lane around the cube
-    // tests of box boundaries; media + nested-BVH kernels keep the second walk, with which
-    // they have the registers.)
-    double ray_len = 0.0;
-    if constexpr (REUSE) ray_len = sqrt(len2(r.d));
+    // are counted.  (Without it media kernels spill 12-20 B/lane around the cube tests of
+    // box boundaries.)
+    const double ray_len = sqrt(len2(r.d));
     LeafHit b1;
     b1.hit = false;
     b1.t = DMAX;
@@ -691,12 +659,7 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
     const uint32_t shape = walk_chain<UNI>(sc, md.boundary, rb, cnt);
     shape_test<UNI>(sc, qs, shape, rb, -DMAX, DMAX, GS_REF_NONE, b1, cnt);
     if (!b1.hit) return;
-    if constexpr (REUSE) {
-        chain_count<UNI>(sc, md.boundary, cnt);
-    } else {
-        rb = r;
-        walk_chain<UNI>(sc, md.boundary, rb, cnt);
-    }
+    chain_count<UNI>(sc, md.boundary, cnt);
     LeafHit b2;
     b2.hit = false;
     b2.t = DMAX;
@@ -707,7 +670,6 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
     if (t2 > closest) t2 = closest;
     if (t1 >= t2) return;
     if (t1 < 0.0) t1 = 0.0;
-    if constexpr (!REUSE) ray_len = sqrt(len2(r.d));
     const double dist_inside_boundary = (t2 - t1) * ray_len;
     const double hit_dist = sp<UNI>(mp)->density_neg_inv * log(wy_f64(rng));
     if (hit_dist > dist_inside_boundary) return;
@@ -717,136 +679,29 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
     res.inst = inst_ref;
 }
 
-// A BVH under a Translate/RotateY chain (final_scene's rotated box of balls, main.rs:
-// 741-755): BVHNode::hit (BVH.rs:69-90) on the ray in the instance's space, as the same
-// left-first walk with a shrinking closest t as the top level.  Like the top level, the
-// nested tree is threaded on the host: its pre-order records (one per node, one per leaf
-// occurrence) with a hit / next link and a miss link, so the walk is `cur = hit ? hit_link
-// : miss_link` with no stack (round 2's private stack cost these instantiations 216 B/lane
-// of scratch).  And like the top level, a node is decided by the certified f32 test on a
-// 32-B record (TNode: f32 box, hit link, miss link; a leaf: NREC_LEAF | next, ABI ref),
-// with the reference's f64 test (DNode) only where f32 cannot decide or the ray is not a
-// cert ray (round 3: half the bytes per node and fewer registers than the f64 walk).
-// `root`: the tree's first record.  Leaves are lists or primitives (validated).
-#define NREC_LEAF 0x80000000u
-// A nested leaf: in kernels for scenes whose nested leaves are all stationary spheres (the
-// box of balls, main.rs:741-755; GS_FEAT_NSPH), Sphere::hit directly, with no kind
-// dispatch; else the generic test.  (A runtime branch between the two, and |d|^2 hoisted
-// out of the walk, spilled 8-16 B/lane.)
-template <bool SPH, bool LC>
-__device__ __forceinline__ void nested_leaf(const DevScene& sc, const QuadSrc& qs, const u32x4& a, const u32x4& b,
-                                            const Ray& r, double tmin, double closest, uint32_t inst_ref, LeafHit& res,
-                                            unsigned long long* cnt, uint32_t& n_sph) {
-    if constexpr (SPH) {
-        // the sphere inline in the leaf record (set up with the nested records): its centre
-        // in the record's first 24 B, its index in the ref's index bits, its radius's slot
-        // in the scene's radius table in the ref's kind bits (the kind is a sphere here)
-        if constexpr (LC) n_sph++;
-        else atomicAdd(&cnt[C_SPH], 1ull);
-        // (a wave whose lanes share the radius slot -- one radius in the scene: always --
-        // reads it with a scalar load)
-        const uint32_t slot = b.w >> GS_REF_SHIFT, s0 = __builtin_amdgcn_readfirstlane(slot);
-        const double rad = __builtin_amdgcn_ballot_w64(slot != s0) == 0 ? sp<true>(sc.nradii)[s0] : sp<false>(sc.nradii)[slot];
-        double t;
-        if (sphere_accept(mk(lo_hi(a.x, a.y), lo_hi(a.z, a.w), lo_hi(b.x, b.y)), rad, r, len2(r.d), tmin, closest, t)) {
-            res.hit = true;
-            res.t = t;
-            res.ref = GS_MAKE_REF(GS_REF_SPHERE, b.w & GS_REF_MASK);
-            res.inst = inst_ref;
-        }
-    } else {
-        shape_test<false>(sc, qs, b.w, r, tmin, closest, inst_ref, res, cnt);
-    }
-}
-template <bool SPH, bool LC>
-__device__ __forceinline__ void nested_bvh(const DevScene& sc, const QuadSrc& qs, uint32_t root, const Ray& r, double tmin,
-                                           double closest, uint32_t inst_ref, LeafHit& res,
-                                           unsigned long long* cnt) {
-    bool fast;
-    RayCert c;
-    {
-        // AABB::hit's `1.0 / ray.direction[axis]` (AABB.rs:64), once per walk (same value)
-        const d3 inv = mk(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
-        fast = sc.nested_cert && cert_ray_ok(r.o, inv);
-        c = make_cert(r.o, inv);
-    }
-    float closest32 = (float)closest;
-    uint32_t cur = root;
-    // (LC: the walk's node visits and sphere tests counted in registers and added to the
-    // block's counters once per walk -- per visit, the LDS atomic and its wave reduction
-    // cost ~4 SALU and 3 VALU.  Not in the media + sphere-run kernels, which spill with it.)
-    uint32_t n_nodes = 0, n_sph = 0;
-    auto count_node = [&]() __attribute__((always_inline)) {
-        if constexpr (LC) n_nodes++;
-        else atomicAdd(&cnt[C_NODES], 1ull);
-    };
-    // (the walk as while-while -- node steps until every lane is at a leaf, then the leaves
-    // together -- measured neutral on final_scene)
-#pragma unroll 1
-    while (cur != THR_END) {
-        u32x4 a, b;
-        // (a scalar branch to the LDS reads when every active lane's record is mirrored)
-        if (__builtin_amdgcn_ballot_w64(cur >= qs.n_nlds) == 0) {
-            a = *(lds_u32x4*)(qs.nlds + cur * 32u);
-            b = *(lds_u32x4*)(qs.nlds + cur * 32u + 16u);
-        } else {
-            const u32x4* q = sp<false>(reinterpret_cast<const u32x4*>(sc.nrecs + cur));
-            a = q[0];
-            b = q[1];
-        }
-        if (b.z & NREC_LEAF) {  // a leaf occurrence: test it, then the next record
-            nested_leaf<SPH, LC>(sc, qs, a, b, r, tmin, closest, inst_ref, res, cnt, n_sph);
-            if (res.hit) {  // res.t only ever shrinks
-                closest = res.t;
-                closest32 = (float)res.t;
-            }
-            cur = b.z & ~NREC_LEAF;
-        } else {
-            count_node();
-            bool h = false, undecided = true;
-            if (fast)
-                h = box_cert(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(b.x), __uint_as_float(a.z),
-                             __uint_as_float(a.w), __uint_as_float(b.y), c, 0.001f, closest32, undecided);
-            if (undecided) h = box_hit_v(ld_node_g(sc.nodes + cur), r.o, inv_of(r.d), tmin, closest);
-#ifdef GS_CERT_CHECK
-            // diagnostic build: every certified nested decision re-checked in f64; mismatches
-            // counted in the block's slot 15 (flushed to counters[15], tools/diag_cert.py)
-            if (fast && !undecided && box_hit_v(ld_node_g(sc.nodes + cur), r.o, inv_of(r.d), tmin, closest) != h)
-                atomicAdd(&cnt[15], 1ull);
-#endif
-            cur = h ? b.z : b.w;
-        }
-    }
-    if constexpr (LC) {
-        atomicAdd(&cnt[C_NODES], (unsigned long long)n_nodes);
-        if constexpr (SPH) atomicAdd(&cnt[C_SPH], (unsigned long long)n_sph);
-    }
-    (void)n_sph;
-    (void)n_nodes;
-}
-
 // The rarer non-node children (everything but a stationary sphere reached directly
-// from a BVH node): moving sphere, quad, triangle, HittableList, ConstantMedium, a BVH
-// under an instance, behind an optional Translate/RotateY chain.  `rng`: a medium draws
-// from the lane's stream.  FEAT (GS_FEAT_*) is a kernel template argument: scenes
-// without media / nested BVHs compile those out (the medium test costs the traversal
-// loop 4 VGPRs and spills otherwise; the nested walk uses private memory).
+// from a BVH node): moving sphere, quad, triangle, HittableList, ConstantMedium, behind an
+// optional Translate/RotateY chain.  `rng`: a medium draws from the lane's stream.  FEAT
+// (GS_FEAT_*) is a kernel template argument: scenes without media compile the medium
+// test out (it costs the traversal loop 4 VGPRs and spills otherwise).
+// A chain that ends in a BVH (GS_FEAT_NESTED: final_scene's box of balls, main.rs:741-755)
+// is not walked here: `r` is left in the tree's space and `enter` = tree + 1, and the
+// caller walks the tree in the main loop's passes (round 5; see the leaf pass).
 template <int FEAT, bool UNI>
-__device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, const QuadSrc& qs, uint32_t ref, Ray r, double tmin,
+__device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, const QuadSrc& qs, uint32_t ref, Ray& r, double tmin,
                                            double closest, uint64_t& rng, unsigned long long* cnt) {
     LeafHit res;
     res.hit = false;
     res.t = closest;
     res.ref = GS_REF_NONE;
     res.inst = GS_REF_NONE;
+    res.enter = 0;
     const uint32_t inst_ref = (ref >> GS_REF_SHIFT) == GS_REF_INSTANCE ? ref : GS_REF_NONE;
     const uint32_t cur = walk_chain<UNI>(sc, ref, r, cnt);
     if ((FEAT & GS_FEAT_MEDIA) && (cur >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
-        medium_test<UNI, (FEAT & GS_FEAT_NESTED) == 0>(sc, qs, cur, r, tmin, closest, inst_ref, rng, res, cnt);
+        medium_test<UNI>(sc, qs, cur, r, tmin, closest, inst_ref, rng, res, cnt);
     } else if ((FEAT & GS_FEAT_NESTED) && (cur >> GS_REF_SHIFT) == GS_REF_NODE) {
-        nested_bvh<(FEAT & GS_FEAT_NSPH) != 0,
-                   (FEAT & (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)) != (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)>(
-            sc, qs, cur & GS_REF_MASK, r, tmin, closest, inst_ref, res, cnt);
+        res.enter = (cur & GS_REF_MASK) + 1u;
     } else {
         shape_test<UNI>(sc, qs, cur, r, tmin, closest, inst_ref, res, cnt);
     }
@@ -1352,7 +1207,14 @@ __host__ __device__ constexpr uint32_t lane_nd(bool chunked, int feat) {
 // ... and the hit primitive's ref (written by leaf tests, read by the shade pass) in one
 // more u32 field, L_HREF.
 enum { L_HREF = L_NI };
-__host__ __device__ constexpr uint32_t lane_ni(int feat) { return (uint32_t)L_NI + (t_in_lds(feat) ? 1u : 0u); }
+// ... and, in kernels that walk BVHs under instances (GS_FEAT_NESTED), the instance chain
+// whose tree the lane walks (GS_REF_NONE at the top level) in one more, L_NINST (not the
+// placement pilot's: it launches with the scene's own lane layout and keeps it in a register).
+__host__ __device__ constexpr bool ninst_in_lds(int feat) {
+    return (feat & GS_FEAT_NESTED) != 0 && (feat & GS_FEAT_VISITS) == 0;
+}
+__host__ __device__ constexpr uint32_t lane_ninst(int feat) { return (uint32_t)L_NI + (t_in_lds(feat) ? 1u : 0u); }
+__host__ __device__ constexpr uint32_t lane_ni(int feat) { return lane_ninst(feat) + (ninst_in_lds(feat) ? 1u : 0u); }
 __host__ __device__ constexpr size_t lane_lds_bytes(bool chunked, int feat) {
     return (size_t)GS_BLOCK * (lane_nd(chunked, feat) * 8 + lane_ni(feat) * 4) + 128 + GS_STAMP_LDS;
 }
@@ -1384,18 +1246,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         src = reinterpret_cast<const uint4*>(A.tquads);
         dst = reinterpret_cast<uint4*>(s_quads);
         for (uint32_t k = threadIdx.x; k < A.lds_quads * 8u; k += GS_BLOCK) dst[k] = src[k];
-        if constexpr ((FEAT & GS_FEAT_NESTED) != 0) {
-            src = reinterpret_cast<const uint4*>(A.nrecs);
-            dst = reinterpret_cast<uint4*>(s_quads + (size_t)A.lds_quads * sizeof(TQuad));
-            for (uint32_t k = threadIdx.x; k < A.lds_nrecs * 2u; k += GS_BLOCK) dst[k] = src[k];
-        }
         src = reinterpret_cast<const uint4*>(A.cubes);
-        dst = reinterpret_cast<uint4*>(s_quads + (size_t)A.lds_quads * sizeof(TQuad) + (size_t)A.lds_nrecs * sizeof(TNode));
+        dst = reinterpret_cast<uint4*>(s_quads + (size_t)A.lds_quads * sizeof(TQuad));
         for (uint32_t k = threadIdx.x; k < A.lds_cubes * (GS_CUBE_DOUBLES / 2); k += GS_BLOCK) dst[k] = src[k];
     }
-    uint8_t* s_nrecs = s_quads + (size_t)A.lds_quads * sizeof(TQuad);
-    uint8_t* s_cubes = s_nrecs + (size_t)A.lds_nrecs * sizeof(TNode);
-    const QuadSrc qs{s_quads, A.tquads, A.lds_quads, s_nrecs, A.lds_nrecs, s_cubes, A.lds_cubes};
+    uint8_t* s_cubes = s_quads + (size_t)A.lds_quads * sizeof(TQuad);
+    const QuadSrc qs{s_quads, A.tquads, A.lds_quads, s_cubes, A.lds_cubes};
     // Per-lane pixel / path state after the mirror: [L_ND][GS_BLOCK] f64, [L_NI][GS_BLOCK] u32.
     double* s_d = (double*)(s_cubes + (size_t)A.lds_cubes * (GS_CUBE_DOUBLES * 8));
     uint32_t* s_i = (uint32_t*)(s_d + A.lane_nd * GS_BLOCK);
@@ -1414,8 +1270,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     const uint32_t tid = threadIdx.x;
     const uint64_t flushers = __builtin_amdgcn_ballot_w64(tid < GS_CNT_SLOTS);  // the counters' flushing lanes
     const double tmin = 0.001;
-    // BVHs under instances keep round 1's advance / begin_ray sites (see the shade pass)
-    constexpr bool kOldSites = (FEAT & GS_FEAT_NESTED) != 0;
     constexpr int kUnroll = unroll_steps(FEAT);  // node steps of an unrolled node pass
     // Every top-level leaf a stationary sphere: no instance is ever hit, so the hit's
     // instance (lane state L_HINST) stays GS_REF_NONE from the kernel's start.
@@ -1424,6 +1278,11 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #define LD(k) s_d[((k) + (t_in_lds(FEAT) ? 3 : 0)) * GS_BLOCK + tid]
 #define LI(k) s_i[(k) * GS_BLOCK + tid]
     if constexpr (kSphLeaf) LI(L_HINST) = GS_REF_NONE;
+    // GS_FEAT_NESTED: the instance chain whose BVH the lane walks (GS_REF_NONE: the top level)
+    constexpr bool kNested = (FEAT & GS_FEAT_NESTED) != 0;
+    uint32_t ninst_ = GS_REF_NONE;
+#define LNINST (*(ninst_in_lds(FEAT) ? &s_i[lane_ninst(FEAT) * GS_BLOCK + tid] : &ninst_))
+    if constexpr (kNested) LNINST = GS_REF_NONE;
 
     uint32_t st = S_NEED;
     bool qdone = false;
@@ -1654,6 +1513,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     uint64_t dist_ref = 0, dist_kind = 0;  // stamps build: distinct leaf refs / ref kinds per leaf pass
     uint64_t dist_bad = 0;                 // stamps build: those counts' loops that did not converge
     uint64_t it_all = 0, it_node = 0, it_leaf = 0, ln_node = 0, ln_leaf = 0, it_shade = 0, ln_shade = 0;
+    uint64_t it_adv = 0, ln_adv = 0;  // stamps build: camera-ray (advance) executions and their lanes
     // stamps build: node steps (lanes) from global memory; wave node steps with any active lane,
     // with any lane reading its record from global memory; active lanes over those steps
     uint64_t d_gvis = 0, d_wsteps = 0, d_wsteps_g = 0, d_wlanes = 0;
@@ -1831,13 +1691,11 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                             LI(L_SAMPLE) = 0u;
                         }
                         st = S_CAM;
-                        if constexpr (kOldSites) advance();  // (see the shade pass)
                     }
                 }
             }
             need = __builtin_amdgcn_ballot_w64(st == S_NEED);
         }
-        if constexpr (kOldSites) break;
         // Camera rays in batches (round 5): get_ray's draws, the defocus rejection loop and
         // the stream seed cost a wave as much for a few lanes as for all 64, and after a
         // shade pass only the lanes whose sample ended (~20 of 57 on C4) want one.  So a
@@ -1847,6 +1705,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         const uint64_t cam_m = __builtin_amdgcn_ballot_w64(st == S_CAM);
         if (cam_m != 0 && ((uint32_t)__popcll(cam_m) >= (uint32_t)A.cam_batch || qdone ||
                            __builtin_amdgcn_ballot_w64(st == S_TRACE) == 0)) {
+#ifdef GS_STAMPS
+            it_adv++;
+            ln_adv += (uint64_t)__popcll(cam_m);
+#endif
             if (st == S_CAM) {
                 GS_MARK("adv_begin");
                 advance();
@@ -1868,7 +1730,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         // shade count and the slab flavour are wave-uniform SGPR facts: no per-iteration
         // ballot for the former, a scalar branch (no exec-mask juggling) for the latter.
         const uint64_t alive = __builtin_amdgcn_ballot_w64(st != S_DONE);
-        const bool wave_fast = __builtin_amdgcn_ballot_w64(st == S_TRACE && !fast) == 0;
+        // (GS_FEAT_NESTED: a lane's ray changes when it enters or leaves a BVH under an
+        // instance, in a leaf pass: recomputed there)
+        bool wave_fast = __builtin_amdgcn_ballot_w64(st == S_TRACE && !fast) == 0;
         // Invariant: cur != THR_END exactly for lanes whose ray is still being traced
         // (every other lane holds THR_END), so the loop reads lane states from `cur` alone
         // and only marks finished lanes S_SHADE once it ends.
@@ -2019,6 +1883,18 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     for (int nstep = 0; nstep < A.node_steps; nstep++) node_step(slow_t{}, mixed_t{});
                 }
                 GS_MARK("node_end");
+            } else if (kNested && __builtin_amdgcn_ballot_w64(cur == THR_RET) != 0) {
+                // Return passes (GS_FEAT_NESTED): a lane whose walk of a BVH under an instance
+                // chain ended (the tree's last links are THR_RET) takes back its top-level ray
+                // and goes on at the record after the instance's leaf -- where BVHNode::hit's
+                // recursion returns from the Translate / RotateY's hit (hittable.rs:107-211).
+                if (cur == THR_RET) {
+                    const double* sv = P->nest_save + ((size_t)blockIdx.x * GS_BLOCK + tid) * 8u;
+                    ray.o = mk(sv[0], sv[1], sv[2]);
+                    ray.d = mk(sv[3], sv[4], sv[5]);
+                    cur = (uint32_t)__double_as_longlong(sv[6]);
+                    LNINST = GS_REF_NONE;
+                }
             } else if (at_leaf) {
                 GS_MARK("leaf_begin");
                 double scx, scy, scz, sr;
@@ -2051,17 +1927,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 }
 #ifdef GS_STAMPS
                 {  // counted by the pass's first active lane (summed over lanes at the end)
-                    // The r03 hang of this build on media scenes was in these counts.  Round-4
-                    // probes (profiles/r04/stamps_hang_probes.txt): waiting for every load first
-                    // did not help (still hung), bounding the loops did, and the bounded runs
-                    // showed the distinct-REF loop converging (cornell_smoke: 1.00 distinct refs
-                    // per pass) while a second loop over the refs' KINDS, the same ballot/readlane
-                    // pattern on `ref >> GS_REF_SHIFT`, did not (16.8 "kinds" where every lane
-                    // held one ref): its compare never matched the lane it read in the media
-                    // kernels (SGPRs spilled to VGPR lanes there), so its mask never emptied.  The
-                    // kinds are now collected from the converging loop's uniform refs, the picked
-                    // lane is always retired (<= 64 steps whatever a ballot returns), and a pass
-                    // whose ballot missed its own lane is counted in dbg[23].
+                    // The r03 hang of this build on media scenes was in these counts: its
+                    // distinct-KIND loop took `readlane(ref, L) >> GS_REF_SHIFT`, and the builtin
+                    // returns int, so the scalar shift was arithmetic while each lane's
+                    // `ref >> GS_REF_SHIFT` was logical: a medium's ref (kind 8, bit 31) never
+                    // matched its own lane and the mask never emptied (ISA:
+                    // profiles/r05/ballot_anomaly_isa.txt).  The readlane results are uint32_t
+                    // here, the kinds come from the ref loop, and the picked lane is retired
+                    // whatever the ballot returns; dbg[23] counts passes whose ballot missed it.
                     const uint64_t act = __builtin_amdgcn_read_exec();
                     const bool first = __builtin_ctzll(act) == (uint32_t)lane;
                     bool bad = false;
@@ -2084,11 +1957,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     GS_MARK("sphere_begin");
                     count_sph();
                     double t;
-                    if (sphere_accept(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
+                    if (sphere_accept_rr(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
                         closest = t;
                         closest32 = (float)t;
                         hit_ref = ref;
-                        if constexpr (!kSphLeaf) LI(L_HINST) = GS_REF_NONE;
+                        if constexpr (kNested) LI(L_HINST) = LNINST;  // (a sphere of the tree under LNINST)
+                        else if constexpr (!kSphLeaf) LI(L_HINST) = GS_REF_NONE;
                     }
                     GS_MARK("sphere_end");
                 };
@@ -2111,8 +1985,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     // lane whose sphere 1 is real takes it against `closest`, then sphere 2
                     // against what it left; a lane whose sphere 1 is not real takes sphere 2
                     // first, as the reference, whose sphere-1 test changed nothing.
-                    const SphereDisc q1 = sphere_disc(mk(scx, scy, scz), sr, ray, a);
-                    const SphereDisc q2 = sphere_disc(mk(s2x, s2y, s2z), s2r, ray, a);
+                    const SphereDisc q1 = sphere_disc_rr(mk(scx, scy, scz), sr, ray, a);
+                    const SphereDisc q2 = sphere_disc_rr(mk(s2x, s2y, s2z), s2r, ray, a);
                     const bool real1 = !(q1.disc < 0.0), real2 = two && !(q2.disc < 0.0);
                     GS_MARK("sphere_begin");
                     double t;
@@ -2159,13 +2033,36 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     const uint32_t r0 = __builtin_amdgcn_readfirstlane(ref);
                     const bool uni = __builtin_amdgcn_ballot_w64(ref != r0) == 0;
                     LeafHit lh;
-                    if (uni) lh = leaf_other<FEAT, true>(sc, qs, r0, ray, tmin, closest, rng, s_cnt);
-                    else lh = leaf_other<FEAT, false>(sc, qs, ref, ray, tmin, closest, rng, s_cnt);
+                    Ray rl = ray;  // (the ray in the leaf's space after its instance chain)
+                    if (uni) lh = leaf_other<FEAT, true>(sc, qs, r0, rl, tmin, closest, rng, s_cnt);
+                    else lh = leaf_other<FEAT, false>(sc, qs, ref, rl, tmin, closest, rng, s_cnt);
                     if (lh.hit) {
                         closest = lh.t;
                         closest32 = (float)lh.t;
                         hit_ref = lh.ref;
-                        LI(L_HINST) = lh.inst;
+                        // (a primitive or list in the tree under LNINST; an instance leaf's own chain)
+                        if constexpr (kNested) LI(L_HINST) = lh.inst != GS_REF_NONE ? lh.inst : LNINST;
+                        else LI(L_HINST) = lh.inst;
+                    }
+                    if constexpr (kNested) {
+                        // The chain ended in a BVH (final_scene's box of balls): the lane walks
+                        // the tree in the main loop's node and leaf passes, in the reference's
+                        // order, with its ray in the tree's space; the top-level ray and the
+                        // link after this leaf wait in the lane's save slot until THR_RET.
+                        if (lh.enter) {
+                            double* sv = P->nest_save + ((size_t)blockIdx.x * GS_BLOCK + tid) * 8u;
+                            sv[0] = ray.o.x;
+                            sv[1] = ray.o.y;
+                            sv[2] = ray.o.z;
+                            sv[3] = ray.d.x;
+                            sv[4] = ray.d.y;
+                            sv[5] = ray.d.z;
+                            sv[6] = __longlong_as_double((long long)next);
+                            LNINST = ref;
+                            ray.o = rl.o;
+                            ray.d = rl.d;
+                            next = sc.nroots[lh.enter - 1u];
+                        }
                     }
                     GS_REGION(7 + (kk_ < 1u ? 1u : kk_ > 8u ? 8u : kk_), k0_);
                     GS_MARK("other_end");
@@ -2181,7 +2078,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 // instances) lose ~2% to the loop's mere presence (MI355X C3).
 #pragma unroll 1
                 for (int k = 1; (FEAT & GS_FEAT_LEAFRUN) && (FEAT & GS_FEAT_SPHLEAF) == 0 &&
-                                k < GS_LEAF_RUN && cur > THR_END; k++) {
+                                k < GS_LEAF_RUN && cur > THR_END && (!kNested || cur != THR_RET); k++) {
                     load_tleaf<(FEAT & GS_FEAT_LDSTREE) != 0>(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr,
                                                          next, ref);
                     if ((FEAT & GS_FEAT_SPHLEAF) == 0 && (ref >> GS_REF_SHIFT) != GS_REF_SPHERE) break;
@@ -2190,11 +2087,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                     count_sph();
                     double t;
-                    if (sphere_accept(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
+                    if (sphere_accept_rr(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
                         closest = t;
                         closest32 = (float)t;
                         hit_ref = ref;
-                        if constexpr (!kSphLeaf) LI(L_HINST) = GS_REF_NONE;
+                        if constexpr (kNested) LI(L_HINST) = LNINST;
+                        else if constexpr (!kSphLeaf) LI(L_HINST) = GS_REF_NONE;
                     }
                     cur = next;
                 }
@@ -2207,11 +2105,17 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             // need the registers (without it these spill 12-36 B/lane).  Media-only kernels
             // (cornell_smoke: a leaf pass after nearly every single node step) have the
             // registers and skip the recomputation (with it: -6.6%).
+            // In nested-BVH kernels a lane's ray also changes in a leaf pass (entering or leaving a
+            // BVH under an instance): its slab flavour is decided again, and the wave's.
             if constexpr ((FEAT & GS_FEAT_NESTED) != 0 ||
                           (FEAT & (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)) == (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)) {
                 if (leaf_pass) {
                     const d3 inv = inv_of(ray.d);
                     rc = make_cert(ray.o, inv);
+                    if constexpr (kNested) {
+                        fast = A.cert_boxes && cert_ray_ok(ray.o, inv);
+                        wave_fast = __builtin_amdgcn_ballot_w64(cur != THR_END && !fast) == 0;
+                    }
                 }
             }
 #ifdef GS_STAMPS
@@ -2316,22 +2220,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             if (ends) {  // the sample is done; its item's next camera ray comes at the loop head
                 GS_STAMP(r0);
                 add_sample(Lr, Lg, Lb);
-                if constexpr (kOldSites) {
-                    // BVHs under instances keep round 1's two advance sites (refill and
-                    // here): with the single site these instantiations spilled 344-376
-                    // B/lane instead of 236 and final_scene ran 16% slower
-                    advance();
-                } else {
-                    if (P->chunk && LI(L_BLEFT) == 0) end_chunk();  // -> S_NEED
-                    else st = S_CAM;
-                }
+                if (P->chunk && LI(L_BLEFT) == 0) end_chunk();  // -> S_NEED
+                else st = S_CAM;
                 GS_REGION(4, r0);
-            }
-        }
-        if constexpr (kOldSites) {  // (round 1's begin_ray site too)
-            if (fresh) {
-                begin_ray();
-                fresh = false;
             }
         }
 #ifdef GS_STAMPS
@@ -2368,11 +2259,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         atomicAdd(&dbg[20], (unsigned long long)d_wsteps);
         atomicAdd(&dbg[21], (unsigned long long)d_wsteps_g);
         atomicAdd(&dbg[22], (unsigned long long)d_wlanes);
+        atomicAdd(&dbg[32], (unsigned long long)it_adv);
+        atomicAdd(&dbg[33], (unsigned long long)ln_adv);
 
     }
 #endif
 #undef LD
 #undef LI
+#undef LNINST
 #undef Tr
 #undef Tg
 #undef Tb
@@ -2634,7 +2528,7 @@ static std::atomic<int32_t> g_cam_batch{0};  // 0: the scene's own (gs_set_camer
 #define GS_KIND_SHADE_BATCH 44
 #endif
 #ifndef GS_KIND_LEAF_BATCH
-#define GS_KIND_LEAF_BATCH 48
+#define GS_KIND_LEAF_BATCH 24
 #endif
 #ifndef GS_KIND_NODE_STEPS
 #define GS_KIND_NODE_STEPS 8
@@ -2704,6 +2598,9 @@ struct LaunchSlot {
     // batch rounds (adaptive settings): round counts, the two active lists, the running sums
     void* rbuf = nullptr;
     size_t rbuf_bytes = 0;
+    // GS_FEAT_NESTED: each lane's save slot (KParams::nest_save), 64 B per lane of the grid
+    double* nest_save = nullptr;
+    size_t nest_save_bytes = 0;
 };
 static const int kLaunchSlots = 4;
 
@@ -2732,9 +2629,12 @@ struct gs_device_scene {
     const TQuad* tquads = nullptr;  // every quad's traversal record, gs_quad order
     uint32_t thr_root = THR_END;
     uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0;  // mirrored prefixes (per block)
-    uint32_t n_nrecs = 0, lds_nrecs = 0;  // nested trees' records, and the mirrored prefix of them
+    // BVHs under instance chains, threaded into the node / leaf arrays with the top-level
+    // tree: each tree's root record (tree index -> record of ThreadedTree), and the device
+    // array of their links (DevScene::nroots), rewritten with the records at re-placement
+    std::vector<uint32_t> nroot_rec;
+    uint32_t* nroots = nullptr;
     uint32_t n_cubes = 0, lds_cubes = 0;  // Quad::cube records (cube_test), and the mirrored prefix
-    const TNode* nrecs = nullptr;
     int32_t node_steps = GS_NODE_STEPS;      // node steps per node pass (from the tree's shape)
     int32_t leaf_batch = 12;                 // lanes at a leaf before a leaf pass (scene's choice)
     int32_t shade_batch = 52;                // finished lanes a wave shades together (scene's choice)
@@ -2749,7 +2649,7 @@ struct gs_device_scene {
     // instantiation (feat minus GS_FEAT_LDSTREE when the mirror is a strict prefix), blocks/CU.
     struct LaunchCfg {
         bool ready = false;
-        uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_nrecs = 0, lds_cubes = 0;
+        uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_cubes = 0;
         size_t lds = 0;
         int feat = 0, per_cu = 0;
     } lcfg[2];
@@ -2787,7 +2687,8 @@ struct Placed {
     std::vector<TBox> tboxes;
     std::vector<TLeaf> tleaves;
     std::vector<uint32_t> pos;  // tree record -> its position in tnodes / tleaves
-    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_nrecs = 0, lds_cubes = 0, root = THR_END;
+    std::vector<uint32_t> nroots;  // the links of the nested trees' roots (DevScene::nroots)
+    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_cubes = 0, root = THR_END;
 };
 // Order the records by how likely a ray tests them and fill the block's LDS byte budget in
 // that order (32-B node records, 48-B leaf records; quads take the rest).  `visits` (one
@@ -2868,9 +2769,13 @@ static bool cube_record(const gs_flat_scene& s, const gs_list& l, uint32_t& q0, 
     return true;
 }
 
+// Raw links of ThreadedTree records: a record index, or the end of the top-level walk, or
+// the end of a nested tree's walk (THR_END / THR_RET once placed).
+#define RAW_END 0xFFFFFFFFu
+#define RAW_RET 0xFFFFFFFEu
 static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* visits,
-                            const std::vector<uint32_t>& single_quads, int64_t budget, uint32_t n_nrecs,
-                            uint32_t n_cubes) {
+                            const std::vector<uint32_t>& single_quads, int64_t budget,
+                            const std::vector<uint32_t>& nroot_rec, uint32_t n_cubes) {
     const uint32_t n = (uint32_t)t.rec.size();
     Placed out;
     std::vector<uint32_t> order(n), pos(n);
@@ -2903,11 +2808,7 @@ static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* 
         top[r] = 1;
         (t.leaf[r] ? out.lds_leaves : out.lds_nodes)++;
     }
-    // then the nested trees' records (shallowest first: they are placed by depth), then quads
-    out.lds_nrecs = GS_NESTED_LDS ? (uint32_t)std::min<int64_t>(n_nrecs, std::max<int64_t>(0, budget - used) /
-                                                                        (int64_t)sizeof(TNode))
-                                  : 0u;
-    used += (int64_t)out.lds_nrecs * (int64_t)sizeof(TNode);
+    // (the nested trees' records are ranked with the top level's: one node / leaf array)
     // a prefix of the quads up to the last quad tested by the quad test that fits (cube-list
     // quads are read from the cube records)
     const int64_t fit = std::max<int64_t>(0, budget - used) / (int64_t)sizeof(TQuad);
@@ -2930,11 +2831,14 @@ static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* 
     out.tnodes.resize(nt_rest);
     out.tboxes.resize(nt_rest);
     out.tleaves.resize(nl_rest);
-    auto tag = [&](uint32_t l) { return l >= n ? THR_END : (t.leaf[l] ? (THR_LEAF | pos[l]) : node_link(pos[l])); };
+    auto tag = [&](uint32_t l) {
+        if (l == RAW_RET) return THR_RET;
+        return l >= n ? THR_END : (t.leaf[l] ? (THR_LEAF | pos[l]) : node_link(pos[l]));
+    };
     for (uint32_t i = 0; i < n; i++) {
         const DNode& r = t.rec[i];
         if (t.leaf[i]) {
-            out.tleaves[pos[i]] = TLeaf{r.mnx, r.mny, r.mnz, r.mxx, tag(r.left), r.right, 0u, 0u};
+            out.tleaves[pos[i]] = TLeaf{r.mnx, r.mny, r.mnz, r.mxx * r.mxx, tag(r.left), r.right, 0u, 0u};
         } else {
             // f32 box coordinates rounded to nearest (the certified test's error model)
             out.tnodes[pos[i]] = TNode{(float)r.mnx, (float)r.mny, (float)r.mxx, (float)r.mxy, (float)r.mnz,
@@ -2943,6 +2847,7 @@ static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* 
         }
     }
     out.root = n == 0 ? THR_END : tag(0);
+    for (uint32_t r : nroot_rec) out.nroots.push_back(tag(r));
     out.pos = std::move(pos);
     return out;
 }
@@ -3254,126 +3159,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     for (uint32_t i = 0; i < s->n_quads; i++)
         if (!in_cube[i]) single_quads.push_back(i);
 
-    // BVHs under instance chains (nested_bvh): each distinct root threaded once into
-    // `nodes` (pre-order records: node {box, hit = next record, miss = after its subtree,
-    // pad0 = 0}, leaf {next, ABI ref, pad0 = 1}; THR_END ends a tree), and the device copy
-    // of the instances points its node children at their tree's first record.
-    std::vector<DNode> nodes;
-    std::vector<TNode> nrecs;  // nodes' f32 records (index-aligned)
-    bool nested_cert = true, nested_sph = true;
-    std::vector<double> nradii;  // the nested spheres' distinct radii (GS_FEAT_NSPH)
     std::vector<gs_instance> insts(s->instances, s->instances + s->n_instances);
-    {
-        std::unordered_map<uint32_t, uint32_t> start;  // node index -> first record
-        std::vector<uint32_t> ndepth;                  // each record's depth in its tree
-        for (size_t ii = 0; ii < insts.size(); ii++) {
-            gs_instance& in = insts[ii];
-            if ((in.child >> GS_REF_SHIFT) != GS_REF_NODE) continue;
-            // Only instances a reachable leaf walks: validate() checked their trees (indices,
-            // depth, leaves); an unreachable one is never read by the kernel and may be
-            // malformed, so its node child is dropped, not walked.
-            if (!inst_reached[ii]) {
-                in.child = GS_REF_NONE;
-                continue;
-            }
-            const uint32_t root = in.child & GS_REF_MASK;
-            auto it = start.find(root);
-            if (it == start.end()) {
-                const uint32_t first = (uint32_t)nodes.size();
-                struct Work {
-                    uint32_t x;
-                    bool close;
-                    uint32_t depth;
-                };
-                std::vector<Work> work{{in.child, false, 0u}};
-                while (!work.empty()) {
-                    const Work w = work.back();
-                    work.pop_back();
-                    if (w.close) {
-                        nodes[w.x].right = (uint32_t)nodes.size();
-                        continue;
-                    }
-                    const uint32_t idx = (uint32_t)nodes.size();
-                    ndepth.push_back(w.depth);
-                    if ((w.x >> GS_REF_SHIFT) == GS_REF_NODE) {
-                        const gs_node& n = s->nodes[w.x & GS_REF_MASK];
-                        nodes.push_back(DNode{n.min[0], n.min[1], n.min[2], n.max[0], n.max[1], n.max[2], idx + 1u, 0u,
-                                              0u, 0u});
-                        work.push_back({idx, true, 0u});
-                        if (n.right != GS_REF_NONE) work.push_back({n.right, false, w.depth + 1u});
-                        work.push_back({n.left, false, w.depth + 1u});
-                    } else {
-                        nodes.push_back(DNode{0, 0, 0, 0, 0, 0, idx + 1u, w.x, 1u, 0u});
-                    }
-                }
-                const uint32_t end = (uint32_t)nodes.size();
-                for (uint32_t k = first; k < end; k++) {
-                    if (nodes[k].left == end) nodes[k].left = THR_END;
-                    if (!nodes[k].pad0 && nodes[k].right == end) nodes[k].right = THR_END;
-                }
-                it = start.emplace(root, first).first;
-            }
-            in.child = GS_MAKE_REF(GS_REF_NODE, it->second);
-        }
-        // Placement of the nested records (GS_NESTED_LDS): shallowest first, so the LDS mirror's
-        // prefix holds every tree's top levels, the records a walk tests most (links are
-        // explicit, so order never changes a walk).
-        if (GS_NESTED_LDS && !nodes.empty()) {
-            const uint32_t n = (uint32_t)nodes.size();
-            std::vector<uint32_t> order(n), npos(n);
-            for (uint32_t k = 0; k < n; k++) order[k] = k;
-            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return ndepth[a] < ndepth[b]; });
-            for (uint32_t k = 0; k < n; k++) npos[order[k]] = k;
-            auto link = [&](uint32_t l) { return l == THR_END ? THR_END : npos[l]; };
-            std::vector<DNode> placed(n);
-            for (uint32_t k = 0; k < n; k++) {
-                DNode d = nodes[k];
-                d.left = link(d.left);                // hit link / next
-                if (!d.pad0) d.right = link(d.right);  // miss link (a leaf's right is its ref)
-                placed[npos[k]] = d;
-            }
-            nodes.swap(placed);
-            for (gs_instance& in : insts)
-                if ((in.child >> GS_REF_SHIFT) == GS_REF_NODE) in.child = GS_MAKE_REF(GS_REF_NODE, npos[in.child & GS_REF_MASK]);
-        }
-        // GS_FEAT_NSPH: every nested leaf a stationary sphere, of at most 16 distinct radii
-        for (const DNode& n : nodes) {
-            if (!n.pad0) continue;
-            if ((n.right >> GS_REF_SHIFT) != GS_REF_SPHERE || (n.right & GS_REF_MASK) >= s->n_spheres) {
-                nested_sph = false;
-                break;
-            }
-            const double rad = s->spheres[n.right & GS_REF_MASK].radius;
-            bool seen = false;
-            for (const double& x : nradii) seen |= std::memcmp(&x, &rad, 8) == 0;
-            if (!seen) nradii.push_back(rad);
-            if (nradii.size() > 16) {
-                nested_sph = false;
-                break;
-            }
-        }
-        if (!GS_NSPH || nodes.empty()) nested_sph = false;
-        if (!nested_sph) nradii.clear();
-        for (const DNode& n : nodes) {  // the f32 records (nested_bvh), index-aligned with nodes
-            if (n.pad0) {
-                TNode t{0, 0, 0, 0, 0, 0, NREC_LEAF | n.left, n.right};
-                if (nested_sph) {  // the sphere inline (nested_leaf)
-                    const gs_sphere& x = s->spheres[n.right & GS_REF_MASK];
-                    uint32_t slot = 0;
-                    while (std::memcmp(&nradii[slot], &x.radius, 8) != 0) slot++;
-                    std::memcpy(&t, x.center, 24);
-                    t.miss = (slot << GS_REF_SHIFT) | (n.right & GS_REF_MASK);
-                }
-                nrecs.push_back(t);
-            } else {
-                nrecs.push_back(TNode{(float)n.mnx, (float)n.mny, (float)n.mxx, (float)n.mxy, (float)n.mnz, (float)n.mxz,
-                                      n.left, n.right});
-                for (double v : {n.mnx, n.mny, n.mnz, n.mxx, n.mxy, n.mxz})
-                    if (!(std::fabs(v) <= 1e15)) nested_cert = false;
-            }
-        }
-        if (nodes.size() > GS_REF_MASK) return fail(GS_ERR_UNSUPPORTED, "more than 2^28 nested BVH records");
-    }
     std::vector<gs_medium> media(s->media, s->media + s->n_media);
     // The threaded top-level tree (see THR_END): pre-order records of nodes and leaf
     // occurrences; raw links first, then split into node and leaf arrays.
@@ -3382,8 +3168,9 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     std::vector<TNode> tnodes;
     std::vector<TBox> tboxes;
     std::vector<TLeaf> tleaves;
-    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_nrecs = 0, lds_cubes = 0, thr_root_tagged = THR_END;
+    uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_cubes = 0, thr_root_tagged = THR_END;
     ThreadedTree tree_keep;  // kept by the scene: re-placed after a launch's pilot (place_records)
+    std::vector<uint32_t> nroot_rec_keep, nroots_placed;  // the nested trees' root records, their links
     std::vector<uint32_t> placed_pos;
     double nodes_per_leaf = 0.0, other_leaf_frac = 0.0;
     bool leaf_runs = false, sph_leaves = false;
@@ -3424,6 +3211,11 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             }
         }
         const uint32_t n = (uint32_t)thr.size();
+        // (the top-level walk's end: RAW_END, so records appended below keep their indices)
+        for (uint32_t i = 0; i < n; i++) {
+            if (thr[i].left >= n) thr[i].left = RAW_END;
+            if (!thr_leaf[i] && thr[i].right >= n) thr[i].right = RAW_END;
+        }
         // Placement: the records a ray is most likely to test first, so a block can mirror
         // them in LDS; the rest in pre-order.  Static estimate (until a launch's pilot
         // measures the real visits, place_records): the smallest surface area of a box on
@@ -3472,17 +3264,132 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                 other_leaf_frac = (thr[0].right >> GS_REF_SHIFT) != GS_REF_SPHERE ? 1.0 : 0.0;
             }
         }
+        // BVHs under instance chains (GS_FEAT_NESTED: final_scene's box of balls, main.rs:
+        // 741-755): each distinct tree under a reached instance is threaded once, in pre-order,
+        // into the same records after the top-level tree -- node {box, hit = next record, miss
+        // = after its subtree}, leaf {a stationary sphere inline, next, ABI ref} -- its last
+        // links RAW_RET (THR_RET: back to the top-level ray); the instance's device child
+        // becomes GS_REF_NODE | tree index, and nroot_rec[tree] its root record.  The lane
+        // walks it in the main loop's node and leaf passes (render kernel, leaf pass), so its
+        // records are placed and mirrored with the top level's by measured visits.
+        {
+            std::unordered_map<uint32_t, uint32_t> tree_of;  // gs node index -> tree
+            std::vector<double> tree_score;                   // a tree's best entry (its leaves' score)
+            std::vector<uint32_t> tree_depth;
+            for (size_t ii = 0; ii < insts.size(); ii++) {
+                gs_instance& in = insts[ii];
+                if ((in.child >> GS_REF_SHIFT) != GS_REF_NODE) continue;
+                // Only instances a reachable leaf walks: validate() checked their trees (indices,
+                // depth, leaves); an unreachable one is never read by the kernel and may be
+                // malformed, so its node child is dropped, not walked.
+                if (!inst_reached[ii]) {
+                    in.child = GS_REF_NONE;
+                    continue;
+                }
+                const uint32_t root = in.child & GS_REF_MASK;
+                auto it = tree_of.find(root);
+                if (it == tree_of.end()) {
+                    const uint32_t first = (uint32_t)thr.size();
+                    struct Work {
+                        uint32_t x;
+                        bool close;
+                    };
+                    std::vector<Work> work{{in.child, false}};
+                    while (!work.empty()) {
+                        const Work w = work.back();
+                        work.pop_back();
+                        if (w.close) {
+                            thr[w.x].right = (uint32_t)thr.size();
+                            continue;
+                        }
+                        const uint32_t idx = (uint32_t)thr.size();
+                        DNode rec{};
+                        if ((w.x >> GS_REF_SHIFT) == GS_REF_NODE) {
+                            const gs_node& nd = s->nodes[w.x & GS_REF_MASK];
+                            rec = DNode{nd.min[0], nd.min[1], nd.min[2], nd.max[0], nd.max[1], nd.max[2], idx + 1u, 0u, 0u, 0u};
+                            thr.push_back(rec);
+                            thr_leaf.push_back(0);
+                            work.push_back({idx, true});
+                            if (nd.right != GS_REF_NONE) work.push_back({nd.right, false});
+                            work.push_back({nd.left, false});
+                        } else {
+                            if ((w.x >> GS_REF_SHIFT) == GS_REF_SPHERE) {
+                                const gs_sphere& q = s->spheres[w.x & GS_REF_MASK];
+                                rec.mnx = q.center[0];
+                                rec.mny = q.center[1];
+                                rec.mnz = q.center[2];
+                                rec.mxx = q.radius;
+                            }
+                            rec.left = idx + 1u;
+                            rec.right = w.x;
+                            thr.push_back(rec);
+                            thr_leaf.push_back(1);
+                        }
+                    }
+                    const uint32_t end = (uint32_t)thr.size();
+                    for (uint32_t k = first; k < end; k++) {
+                        if (thr[k].left == end) thr[k].left = RAW_RET;
+                        if (!thr_leaf[k] && thr[k].right == end) thr[k].right = RAW_RET;
+                    }
+                    it = tree_of.emplace(root, (uint32_t)nroot_rec_keep.size()).first;
+                    nroot_rec_keep.push_back(first);
+                    tree_score.push_back(0.0);
+                    tree_depth.push_back(0);
+                }
+                in.child = GS_MAKE_REF(GS_REF_NODE, it->second);
+            }
+            if (nroot_rec_keep.size() > GS_REF_MASK) return fail(GS_ERR_UNSUPPORTED, "too many BVHs under instances");
+            // Static estimate for the nested records: a top-level leaf whose chain ends in a
+            // tree gives it its score and depth; inside, the smallest surface area on the path
+            // relative to the tree's root box (rigid transforms keep areas).
+            for (uint32_t i = 0; i < n; i++) {
+                if (!thr_leaf[i]) continue;
+                uint32_t r = thr[i].right;
+                for (int k = 0; k < GS_MAX_CHAIN && (r >> GS_REF_SHIFT) == GS_REF_INSTANCE; k++) r = insts[r & GS_REF_MASK].child;
+                if ((r >> GS_REF_SHIFT) != GS_REF_NODE) continue;
+                const uint32_t tr = r & GS_REF_MASK;
+                if (score[i] > tree_score[tr]) {
+                    tree_score[tr] = score[i];
+                    tree_depth[tr] = depth[i] + 1;
+                }
+            }
+            const uint32_t total = (uint32_t)thr.size();
+            depth.resize(total, 0);
+            score.resize(total, 0.0);
+            for (size_t tr = 0; tr < nroot_rec_keep.size(); tr++) {
+                const uint32_t first = nroot_rec_keep[tr];
+                const uint32_t end = tr + 1 < nroot_rec_keep.size() ? nroot_rec_keep[tr + 1] : total;
+                const DNode& rb = thr[first];
+                const double rdx = rb.mxx - rb.mnx, rdy = rb.mxy - rb.mny, rdz = rb.mxz - rb.mnz;
+                const double sa_root = rdx * rdy + rdy * rdz + rdz * rdx;
+                depth[first] = tree_depth[tr];
+                score[first] = tree_score[tr];
+                std::vector<double> local(end - first, sa_root);
+                for (uint32_t i = first; i < end; i++)
+                    if (!thr_leaf[i]) {
+                        const DNode& b = thr[i];
+                        const double dx = b.mxx - b.mnx, dy = b.mxy - b.mny, dz = b.mxz - b.mnz;
+                        const double sa = std::min(local[i - first], dx * dy + dy * dz + dz * dx);
+                        for (uint32_t c = thr[i].left; c < thr[i].right && c < end;) {
+                            depth[c] = depth[i] + 1;
+                            local[c - first] = sa;
+                            score[c] = sa_root > 0.0 ? tree_score[tr] * std::min(1.0, sa / sa_root) : tree_score[tr];
+                            c = thr_leaf[c] ? c + 1 : thr[c].right;
+                        }
+                    }
+            }
+        }
         tree_keep = ThreadedTree{thr, thr_leaf, std::move(depth), std::move(score)};
         const Placed pl = place_records(tree_keep, nullptr, single_quads,
-                                        g_lds_mirror < 0 ? lds_mirror_budget() : g_lds_mirror, (uint32_t)nrecs.size(),
+                                        g_lds_mirror < 0 ? lds_mirror_budget() : g_lds_mirror, nroot_rec_keep,
                                         (uint32_t)(cubes.size() / GS_CUBE_DOUBLES));
+        nroots_placed = pl.nroots;
         tnodes = pl.tnodes;
         tboxes = pl.tboxes;
         tleaves = pl.tleaves;
         lds_nodes = pl.lds_nodes;
         lds_leaves = pl.lds_leaves;
         lds_quads = pl.lds_quads;
-        lds_nrecs = pl.lds_nrecs;
         lds_cubes = pl.lds_cubes;
         thr_root_tagged = pl.root;
         placed_pos = pl.pos;
@@ -3490,10 +3397,12 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         // adjacent sphere leaves (C4's two-sphere leaves of BVH.rs:44-55: ~half).
         {
             auto is_sph = [&](uint32_t i) { return thr_leaf[i] && (thr[i].right >> GS_REF_SHIFT) == GS_REF_SPHERE; };
+            // (over every record: a nested tree's leaf pairs run in the same leaf passes)
+            const uint32_t na = (uint32_t)thr.size();
             uint64_t leaves = 0, pairs = 0;
-            for (uint32_t i = 0; i < n; i++) {
+            for (uint32_t i = 0; i < na; i++) {
                 leaves += thr_leaf[i];
-                pairs += i + 1 < n && is_sph(i) && is_sph(i + 1);
+                pairs += i + 1 < na && is_sph(i) && is_sph(i + 1) && thr[i].left == i + 1;
             }
             leaf_runs = leaves && pairs * 4 >= leaves;
             sph_leaves = leaves > 0;
@@ -3572,9 +3481,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             if (!encode_rgbe(s->hdri_rgb + 3 * k, &rgbe[k])) rgbe.clear();
     }
     Layout L;
-    size_t o_nodes = L.add(nodes.data(), nodes.size() * sizeof(DNode));
-    size_t o_nrecs = L.add(nrecs.data(), nrecs.size() * sizeof(TNode));
-    size_t o_nradii = L.add(nradii.data(), nradii.size() * sizeof(double));
+    size_t o_nroots = L.add(nroots_placed.data(), nroots_placed.size() * 4);
     size_t o_tnodes = L.add(tnodes.data(), tnodes.size() * sizeof(TNode));
     size_t o_tboxes = L.add(tboxes.data(), tboxes.size() * sizeof(TBox));
     size_t o_tleaves = L.add(tleaves.data(), tleaves.size() * sizeof(TLeaf));
@@ -3614,10 +3521,7 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     }
     uint8_t* b = (uint8_t*)ds->mem;
     DevScene& d = ds->dev;
-    d.nodes = (const DNode*)(b + o_nodes);
-    d.nrecs = (const TNode*)(b + o_nrecs);
-    d.nested_cert = nested_cert ? 1u : 0u;
-    d.nradii = (const double*)(b + o_nradii);
+    d.nroots = (const uint32_t*)(b + o_nroots);
     d.spheres = (const DSphere*)(b + o_sph);
     d.sphere_mat = (const uint32_t*)(b + o_sphm);
     d.mspheres = (const gs_msphere*)(b + o_msph);
@@ -3654,19 +3558,17 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     ds->lds_nodes = lds_nodes;
     ds->lds_leaves = lds_leaves;
     ds->lds_quads = lds_quads;
-    ds->lds_nrecs = lds_nrecs;
-    ds->n_nrecs = (uint32_t)nrecs.size();
+    ds->nroot_rec = nroot_rec_keep;
+    ds->nroots = (uint32_t*)(b + o_nroots);
     ds->single_quads = single_quads;
     ds->lds_cubes = lds_cubes;
     ds->n_cubes = (uint32_t)(cubes.size() / GS_CUBE_DOUBLES);
-    ds->nrecs = (const TNode*)(b + o_nrecs);
     ds->node_records = (uint32_t)tnodes.size();
     ds->leaf_records = (uint32_t)tleaves.size();
     ds->nodes_per_leaf = nodes_per_leaf;
     ds->other_leaf_frac = other_leaf_frac;
     ds->bvh_depth = depth < 1 ? 1 : depth;
     ds->feat = (s->n_media != 0 ? GS_FEAT_MEDIA : 0) | (nested ? GS_FEAT_NESTED : 0) | (leaf_runs ? GS_FEAT_LEAFRUN : 0);
-    if (nested && nested_sph) ds->feat |= GS_FEAT_NSPH;
     if (!(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED)) && lds_nodes == tnodes.size() && lds_leaves == tleaves.size())
         ds->feat |= GS_FEAT_LDSTREE;  // (cleared at launch if the device's LDS cannot hold it all)
     {  // staged shading when three or more of its sharing cases can meet in one wave
@@ -3691,11 +3593,13 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     // ... and shade smaller batches (round 4, after the nested-leaf changes; shade batch x leaf
     // batch at 8 node steps, twice: 44 / 48: 2 396, 2 462; 44 / 56: 2 449, 2 453; 52 / 48:
     // 2 365, 2 398 Msamples/s, profiles/r04/sweep_final_scene_shade_leaf_batch.txt).
+    // Round 5 walks the nested BVHs in the main node passes, so a leaf pass holds fewer
+    // leaf kinds and smaller batches pay: leaf batch 48 -> 2 577, 24 -> 2 644-2 660
+    // Msamples/s (profiles/r05).
     if (ds->feat & GS_FEAT_NESTED) {
         ds->leaf_batch = GS_KIND_LEAF_BATCH;
         ds->shade_batch = GS_KIND_SHADE_BATCH;
         ds->node_steps = std::max<int32_t>(ds->node_steps, GS_KIND_NODE_STEPS);
-        if (ds->feat & GS_FEAT_NSPH) ds->node_steps = unroll_steps(ds->feat);  // (the unrolled pass, 16)
     }
     ds->tree = std::move(tree_keep);
     ds->pos = std::move(placed_pos);
@@ -3734,6 +3638,7 @@ gs_status gs_device_scene_destroy(gs_device_scene* ds) {
         }
         if (sl.partial) (void)hipFree(sl.partial);
         if (sl.rbuf) (void)hipFree(sl.rbuf);
+        if (sl.nest_save) (void)hipFree(sl.nest_save);
     }
     if (ds->mem) (void)hipFree(ds->mem);
     delete ds;
@@ -3782,13 +3687,6 @@ static void (*kernel_for(int feat))(KArgs) {
         case GS_FEAT_LEAFRUN | GS_FEAT_NESTED: return gs_render_kernel<GS_FEAT_LEAFRUN | GS_FEAT_NESTED>;
         case GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED:
             return gs_render_kernel<GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED>;
-        case GS_FEAT_NSPH | GS_FEAT_NESTED: return gs_render_kernel<GS_FEAT_NSPH | GS_FEAT_NESTED>;
-        case GS_FEAT_NSPH | GS_FEAT_MEDIA | GS_FEAT_NESTED:
-            return gs_render_kernel<GS_FEAT_NSPH | GS_FEAT_MEDIA | GS_FEAT_NESTED>;
-        case GS_FEAT_NSPH | GS_FEAT_LEAFRUN | GS_FEAT_NESTED:
-            return gs_render_kernel<GS_FEAT_NSPH | GS_FEAT_LEAFRUN | GS_FEAT_NESTED>;
-        case GS_FEAT_NSPH | GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED:
-            return gs_render_kernel<GS_FEAT_NSPH | GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED>;
         case GS_FEAT_LDSTREE: return gs_render_kernel<GS_FEAT_LDSTREE>;
         case GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN: return gs_render_kernel<GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN>;
         case GS_FEAT_MIXED: return gs_render_kernel<GS_FEAT_MIXED>;
@@ -3797,7 +3695,6 @@ static void (*kernel_for(int feat))(KArgs) {
         case GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN:
             return gs_render_kernel<GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN>;
         case GS_FEAT_PILOT: return gs_render_kernel<GS_FEAT_PILOT>;
-        case GS_FEAT_PILOT | GS_FEAT_NSPH: return gs_render_kernel<GS_FEAT_PILOT | GS_FEAT_NSPH>;  // (the inline nested spheres' format)
         case GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN: return gs_render_kernel<GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN>;
         case GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_LDSTREE:
             return gs_render_kernel<GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_LDSTREE>;
@@ -4006,16 +3903,14 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         if (fa.sharedSizeBytes != 0) return fail(GS_ERR_UNSUPPORTED, "render kernel with static LDS");
         const int64_t room = (int64_t)max_lds - (int64_t)lane_lds_bytes(chunked, ds->feat);
         if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
-        uint32_t ln = ds->lds_nodes, ll = ds->lds_leaves, lq = ds->lds_quads, lr = ds->lds_nrecs, lk = ds->lds_cubes;
+        uint32_t ln = ds->lds_nodes, ll = ds->lds_leaves, lq = ds->lds_quads, lk = ds->lds_cubes;
         auto bytes = [&] {
             return (int64_t)ln * (int64_t)sizeof(TNode) + (int64_t)ll * (int64_t)sizeof(TLeaf) +
-                   (int64_t)lq * (int64_t)sizeof(TQuad) + (int64_t)lr * (int64_t)sizeof(TNode) +
-                   (int64_t)lk * (GS_CUBE_DOUBLES * 8);
+                   (int64_t)lq * (int64_t)sizeof(TQuad) + (int64_t)lk * (GS_CUBE_DOUBLES * 8);
         };
-        // shrink the least valuable prefix first: cubes, quads, then nested records, then all
+        // shrink the least valuable prefix first: cubes, quads, then all
         while (bytes() > room && lk) lk = lk - 1 - lk / 16;
         while (bytes() > room && lq) lq = lq - 1 - lq / 16;
-        while (bytes() > room && lr) lr = lr - 1 - lr / 16;
         while (bytes() > room) {
             if (ln) ln = ln - 1 - ln / 16;  // shrink the prefixes until they fit
             if (ll) ll = ll - 1 - ll / 16;
@@ -4023,7 +3918,6 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         lc.lds_nodes = ln;
         lc.lds_leaves = ll;
         lc.lds_quads = lq;
-        lc.lds_nrecs = (ds->feat & GS_FEAT_NESTED) ? lr : 0u;
         lc.lds_cubes = lk;
         lc.lds = lane_lds_bytes(chunked, ds->feat) + (size_t)bytes();
         lc.feat = ds->feat;
@@ -4038,8 +3932,6 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     a.lds_nodes = lc.lds_nodes;
     a.lds_leaves = lc.lds_leaves;
     a.lds_quads = lc.lds_quads;
-    a.lds_nrecs = lc.lds_nrecs;
-    a.nrecs = ds->nrecs;
     a.lds_cubes = lc.lds_cubes;
     a.cubes = ds->dev.cubes;
     a.lane_nd = lane_nd(chunked, ds->feat);
@@ -4124,6 +4016,19 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         kp.active_buf[1] = (uint32_t*)(rb + r_counts + r_list);
         kp.pstate = (double*)(rb + r_counts + 2 * r_list);
     }
+    if (lc.feat & GS_FEAT_NESTED) {  // (and the pilot's instantiation, which has every path)
+        const size_t need = (size_t)blocks * GS_BLOCK * 64u;
+        if (sl.nest_save_bytes < need) {
+            if (sl.used) HIPCHK(hipEventSynchronize(sl.done));
+            if (sl.nest_save) (void)hipFree(sl.nest_save);
+            sl.nest_save = nullptr;
+            sl.nest_save_bytes = 0;
+            if (hipMalloc(&sl.nest_save, need) != hipSuccess)
+                return fail(GS_ERR_OOM, "hipMalloc of " + std::to_string(need) + " bytes of nested-walk save slots failed");
+            sl.nest_save_bytes = need;
+        }
+        kp.nest_save = sl.nest_save;
+    }
     kp.queue = sl.queue;
     a.P = sl.params;
     if (outs->item_visits) HIPCHK(hipMemsetAsync(outs->item_visits, 0, (size_t)cap * sizeof(uint32_t), st));
@@ -4157,7 +4062,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     }
     if (k_begin) HIPCHK(hipEventRecord(k_begin, st));
     const bool pilot_kernel = va != nullptr;
-    hipLaunchKernelGGL(kernel_for(pilot_kernel ? (GS_FEAT_PILOT | (lc.feat & GS_FEAT_NSPH)) : lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
+    hipLaunchKernelGGL(kernel_for(pilot_kernel ? GS_FEAT_PILOT : lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
     if (k_end) HIPCHK(hipEventRecord(k_end, st));
     if (chunk) {
@@ -4247,7 +4152,7 @@ static gs_status pilot_end(gs_device_scene* ds, PilotRun& pr) {
     const ThreadedTree& t = ds->tree;
     std::vector<uint64_t> counts(t.rec.size());
     for (size_t i = 0; i < t.rec.size(); i++) counts[i] = t.leaf[i] ? vis[(size_t)nn + ds->pos[i]] : vis[ds->pos[i]];
-    Placed pl = place_records(t, &counts, ds->single_quads, ds->mirror_budget, ds->n_nrecs, ds->n_cubes);
+    Placed pl = place_records(t, &counts, ds->single_quads, ds->mirror_budget, ds->nroot_rec, ds->n_cubes);
     if (pl.tnodes.size() != nn || pl.tleaves.size() != nl) return fail(GS_ERR_HIP, "placement changed the record counts");
     {
         // The arrays are rewritten in place, so nothing of this scene may be running: the
@@ -4265,11 +4170,12 @@ static gs_status pilot_end(gs_device_scene* ds, PilotRun& pr) {
                          hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(const_cast<TLeaf*>(ds->tleaves), pl.tleaves.data(), pl.tleaves.size() * sizeof(TLeaf),
                          hipMemcpyHostToDevice));
+        if (!pl.nroots.empty())
+            HIPCHK(hipMemcpy(ds->nroots, pl.nroots.data(), pl.nroots.size() * 4, hipMemcpyHostToDevice));
         ds->thr_root = pl.root;
         ds->lds_nodes = pl.lds_nodes;
         ds->lds_leaves = pl.lds_leaves;
         ds->lds_quads = pl.lds_quads;
-        ds->lds_nrecs = pl.lds_nrecs;
         ds->lds_cubes = pl.lds_cubes;
         ds->pos = std::move(pl.pos);
         ds->lcfg[0].ready = ds->lcfg[1].ready = false;  // mirror prefixes changed

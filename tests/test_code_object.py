@@ -33,11 +33,10 @@ def test_product_kernels_have_no_scratch(built):
     """Every kernel the product launches for a render runs without private (scratch)
     memory: register spills in the megakernel cost a memory round trip inside the loop
     (VERDICT r2 item 4).  Read from the kernel descriptors of the built code objects.  The
-    placement pilot's counting instantiations (GS_FEAT_PILOT = 55: every code path, one 1-spp
-    launch per scene; 183 with the nested sphere-leaf format) are the exception, and stay small."""
+    placement pilot's counting instantiation (GS_FEAT_PILOT = 55: every code path, one 1-spp
+    launch per scene) is the exception, and stays small."""
     scratch = codeobj.kernel_scratch(LIB_PATH)
     render = {k: v for k, v in scratch.items() if "gs_render_kernel" in k}
-    assert len(render) >= 24  # 22 product instantiations + the two pilots
-    for pilot in ("_Z16gs_render_kernelILi55EEv5KArgs", "_Z16gs_render_kernelILi183EEv5KArgs"):  # (+ GS_FEAT_NSPH)
-        assert scratch.pop(pilot) <= 64
+    assert len(render) >= 19  # 18 product instantiations + the pilot
+    assert scratch.pop("_Z16gs_render_kernelILi55EEv5KArgs") <= 64
     assert {k: v for k, v in scratch.items() if v} == {}

@@ -33,8 +33,9 @@ def test_scene_matches_oracle(name, width, spp):
 
 def nested_scene(width=40, spp=8, depth_chain=2, leaf="spheres", radii=1):
     """A BVH of spheres / cubes (lists) / triangles under a Translate/RotateY chain,
-    next to top-level geometry.  `radii`: distinct sphere radii (all-sphere trees of at most
-    16 take the inline nested-sphere records, GS_FEAT_NSPH; more take the generic test)."""
+    next to top-level geometry.  `radii`: distinct sphere radii (round 4's inline nested-sphere
+    records took at most 16; since round 5 a nested tree's leaves are ordinary leaf records of
+    the main walk, spheres inline whatever their radii)."""
     b = g.SceneBuilder()
     rng = np.random.default_rng(7)
     white = b.lambertian((0.73, 0.73, 0.73))
@@ -70,9 +71,8 @@ def nested_scene(width=40, spp=8, depth_chain=2, leaf="spheres", radii=1):
 def test_nested_bvh_variants_match_oracle(leaf, radii, depth_chain):
     sc = nested_scene(leaf=leaf, depth_chain=depth_chain, radii=radii)
     r = g.Renderer(sc)
-    nsph = (r.scene_info()["feat"] & 128) != 0  # GS_FEAT_NSPH: the inline nested-sphere records
+    assert r.scene_info()["feat"] & 2  # GS_FEAT_NESTED: the trees are walked in the main loop
     r.close()
-    assert nsph == (leaf == "spheres" and radii <= 16)
     out, gc = g.render(sc, seed=4)
     ref, rc = oracle.render(sc, seed=4)
     assert maxdiff(out, ref) < TOL

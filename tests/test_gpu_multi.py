@@ -268,3 +268,33 @@ def test_frame_context_from_two_threads():
     assert sum(1 for s in seeds if got[s]["stats"]["setup_ms"] > 0.0) == 1
     assert m.scene_info()["placement"] == 2
     m.close()
+
+
+def test_async_launch_returns_while_the_kernel_runs():
+    """the N-device issue loop (multi_gpu.cpp) launches every device's
+    frame before waiting for any, so a launch call must return while its kernel still runs,
+    or the devices would serialise.  After a warm-up frame (the placement pilot and the
+    slot's chunk-sum buffer are in place), the host call of a >= 100 ms C4 launch returns
+    in well under a millisecond, long before the stream drains."""
+    import time
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    sc = scenes.config("C4", width=1920, spp=160)
+    r = g.Renderer(sc, 0, 1, 64)
+    st = torch.cuda.Stream(dev)
+    buf = torch.zeros(r.capacity * 3, dtype=torch.float32, device=dev)
+    r.render_async(buf.data_ptr(), 0, st.cuda_stream, seed=1)  # warm-up: pilot, buffers
+    torch.cuda.synchronize()
+    calls = []
+    for seed in (2, 3):
+        t0 = time.perf_counter()
+        r.render_async(buf.data_ptr(), 0, st.cuda_stream, seed=seed)
+        calls.append(time.perf_counter() - t0)
+        t1 = time.perf_counter()
+        st.synchronize()
+        calls.append(-(time.perf_counter() - t1))  # (negative: the wait, kept apart below)
+    launches = [c for c in calls if c >= 0]
+    waits = [-c for c in calls if c < 0]
+    r.close()
+    assert min(waits) > 0.05, waits  # the frames did run long (>= ~100 ms of kernel)
+    assert max(launches) < 1e-3, launches

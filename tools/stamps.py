@@ -76,7 +76,7 @@ def main():
         "leaf passes": (leaf_clk, ln_leaf / max(1, it_leaf)),
         "shade passes": (v[2], ln_shade / max(1, it_shade)),
     }
-    if it_adv:  # (kernels with BVHs under instances run get_ray per lane in the refill: not counted)
+    if it_adv:
         phases["refill + camera rays (per get_ray)"] = (v[0], ln_adv / it_adv)
     tot_clk = sum(p[0] for p in phases.values())
     lane_frac = sum(p[0] * p[1] / 64.0 for p in phases.values()) / max(1, tot_clk)
