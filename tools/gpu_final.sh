@@ -11,7 +11,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-T=${TAG:-r04_final}
+T=${TAG:-r05_final}
 O=$R/gpurun_out/$T
 mkdir -p $O
 STAGES=${STAGES:-"tests bench pmc stamps configs"}

@@ -19,4 +19,4 @@ for set in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_
   echo "pass $i ok: $set"
 done
 # (PMC_TAG: the summary's name for an overridden size, e.g. final_scene_w1440_s64, bench.py)
-python3 $R/tools/pmc_summary.py $O $R/gpurun_out/pmc_out --config ${PMC_TAG:-$CONFIG} --round 4
+python3 $R/tools/pmc_summary.py $O $R/gpurun_out/pmc_out --config ${PMC_TAG:-$CONFIG} --round ${ROUND:-5}
