@@ -110,6 +110,9 @@ def parse():
     ap.add_argument("--camera-batch", type=int, default=0,
                     help="lanes wanting a camera ray before a wave generates them (0: the scene's choice)")
     ap.add_argument("--sample-chunk", type=int, default=None, help="samples per work item (-1 auto, 0 whole pixel)")
+    ap.add_argument("--fine-chunk", type=int, default=0, help="auto chunks' guided tail: samples per fine chunk (0: default)")
+    ap.add_argument("--tail-pct", type=int, default=0,
+                    help="auto chunks' guided tail: fine samples as %% of lanes x coarse chunk (0: default 200)")
     ap.add_argument("--adaptive-mode", type=int, default=1, choices=[0, 1, 2],
                     help="adaptive settings (gs_set_adaptive_mode): 1 auto (default), 2 batch rounds, 0 the per-lane loop")
     ap.add_argument("--cpu-stride", type=int, default=3,
@@ -147,6 +150,7 @@ def load_scene(a):
                  -1 if a.sample_chunk is None else a.sample_chunk)
     g._native.check(g._native.lib.gs_set_node_steps(a.node_steps))
     g._native.check(g._native.lib.gs_set_camera_batch(a.camera_batch))
+    g._native.check(g._native.lib.gs_debug_set_guided_tail(a.fine_chunk, a.tail_pct))
     g._native.check(g._native.lib.gs_set_adaptive_mode(a.adaptive_mode))
     if a.config in scenes.CONFIGS:
         return scenes.config(a.config, width=a.width, spp=a.spp)

@@ -25,7 +25,7 @@ pub const GS_REF_TRIANGLE: u32 = 5;
 pub const GS_REF_LIST: u32 = 6;
 pub const GS_REF_INSTANCE: u32 = 7;
 pub const GS_REF_MEDIUM: u32 = 8;
-pub const GS_ABI_VERSION: i32 = 9;
+pub const GS_ABI_VERSION: i32 = 10;
 pub const fn gs_make_ref(kind: u32, idx: u32) -> u32 { (kind << GS_REF_SHIFT) | (idx & 0x0FFF_FFFF) }
 
 #[repr(C)] #[derive(Clone, Copy, Default)]
@@ -147,6 +147,7 @@ extern "C" {
     pub fn gs_version() -> i32;
     pub fn gs_set_tuning(shade_batch: i32, blocks_per_cu: i32, leaf_batch: i32, sample_chunk: i32) -> gs_status;
     pub fn gs_debug_set_partial_budget(bytes: u64) -> gs_status;
+    pub fn gs_debug_set_guided_tail(fine_chunk: i32, tail_pct: i32) -> gs_status;
     pub fn gs_set_node_steps(node_steps: i32) -> gs_status;
     pub fn gs_set_camera_batch(cam_batch: i32) -> gs_status;
     pub fn gs_set_placement(mode: i32) -> gs_status;

@@ -16,7 +16,7 @@ GS_OBJ_LIST, GS_OBJ_BVH, GS_OBJ_TRANSLATE, GS_OBJ_ROTATE_Y, GS_OBJ_CUBE, GS_OBJ_
 GS_MAT_LAMBERTIAN, GS_MAT_METAL, GS_MAT_DIELECTRIC, GS_MAT_DIFFUSE_LIGHT, GS_MAT_ISOTROPIC = 1, 2, 3, 4, 5
 GS_TEX_SOLID, GS_TEX_CHECKERED, GS_TEX_IMAGE, GS_TEX_NOISE = 1, 2, 3, 4
 GS_BG_SOLID, GS_BG_HDRI = 1, 2
-GS_ABI_VERSION = 9
+GS_ABI_VERSION = 10
 GS_OK, GS_ERR_ARG, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPORTED, GS_ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5
 
 D3 = C.c_double * 3
@@ -160,6 +160,7 @@ SIGNATURES = {
     "gs_version": (C.c_int32, []),
     "gs_set_tuning": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "gs_debug_set_partial_budget": (C.c_int32, [C.c_uint64]),
+    "gs_debug_set_guided_tail": (C.c_int32, [C.c_int32, C.c_int32]),
     "gs_set_node_steps": (C.c_int32, [C.c_int32]),
     "gs_set_camera_batch": (C.c_int32, [C.c_int32]),
     "gs_set_placement": (C.c_int32, [C.c_int32]),

@@ -168,10 +168,13 @@ struct KParams {
     // samples [(q % cpp) * chunk, +chunk)); each item leaves its Σrgb in `partial` and
     // gs_combine_kernel sums a pixel's chunks in chunk order.  chunk == 0: one item per
     // pixel running the reference's batch loop (camera.rs:135-165) to completion.
+    // `partial` is chunk-major (round 5): chunk ck of coarse pixel k at ck * fine_px + k, of
+    // fine pixel k at fine_base + ck * (capacity - fine_px) + k - fine_px, so the combine's
+    // lanes (consecutive pixels) read consecutive sums.
     uint32_t chunk, cpp, n_items;
     // Guided tail: the packed pixels from fine_px on (the rank's last tiles in queue order)
-    // run in smaller chunks (fine_chunk samples, fine_cpp per pixel), their items from
-    // fine_base = fine_px * cpp on, so the frame's last items are short (fine_px =
+    // run in smaller chunks (fine_chunk samples, fine_cpp per pixel), their items (and
+    // sums) from fine_base = fine_px * cpp on, so the frame's last items are short (fine_px =
     // capacity: no fine region).
     uint32_t fine_px, fine_base, fine_chunk, fine_cpp;
     uint32_t claim;  // work items a wave claims per queue atomic (its private reserve)
@@ -183,6 +186,9 @@ struct KParams {
     double* partial;
     float* out;     // linear colour per packed pixel (nullable when out8 is set)
     uint8_t* out8;  // write_color bytes of the f64 colour per packed pixel (nullable)
+    // 1: out / out8 are the W x H frame itself (image pixel j * W + i), padding slots are not
+    // written -- the one-device frame context, which then needs no unpack (round 5)
+    uint32_t direct;
     unsigned long long* counters;
     uint32_t* queue;
     uint32_t* item_visits;  // diagnostic: node visits per packed pixel (nullable)
@@ -1379,8 +1385,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             o[2] = LD(L_CSB);
         }
 #if !defined(GS_STAMPS) && !defined(GS_CERT_CHECK)  // (those builds use item_visits as their record buffer)
-        if (P->item_visits) {
-            atomicAdd(&P->item_visits[item / P->cpp], c_nodes);
+        if (P->item_visits) {  // (the item's packed pixel, from its chunk-major sum slot)
+            const uint32_t k = item < P->fine_base ? item % P->fine_px
+                                                   : P->fine_px + (item - P->fine_base) % (P->capacity - P->fine_px);
+            atomicAdd(&P->item_visits[k], c_nodes);
             flush_counts();
         }
 #endif
@@ -1407,15 +1415,16 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 if (!stop) stop = (uint32_t)sat_u64(scount, 4294967295.0, 4294967295ull) > P->ss.max_samples;
                 if (stop) {
                     const uint32_t item = LI(L_ITEM);
+                    const size_t oi = P->direct ? (size_t)LI(L_PIX) : (size_t)item;
                     const double cr = LD(L_CSR) / scount, cg = LD(L_CSG) / scount, cb = LD(L_CSB) / scount;
                     if (P->out) {
-                        float* o = P->out + (size_t)item * 3;
+                        float* o = P->out + oi * 3;
                         o[0] = (float)cr;
                         o[1] = (float)cg;
                         o[2] = (float)cb;
                     }
                     if (P->out8) {
-                        uint8_t* o8 = P->out8 + (size_t)item * 3;
+                        uint8_t* o8 = P->out8 + oi * 3;
                         o8[0] = color_byte(cr);
                         o8[1] = color_byte(cg);
                         o8[2] = color_byte(cb);
@@ -1630,7 +1639,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     const uint32_t pi = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu : tx * (uint32_t)P->tile_w + x;
                     const uint32_t pj = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu : ty * (uint32_t)P->tile_h + y;
                     if (pi >= (uint32_t)cam.image_width || pj >= (uint32_t)cam.image_height) {
-                        if (!P->chunk) {  // padding pixel (chunked: gs_combine_kernel writes it)
+                        if (!P->chunk && !P->direct) {  // padding pixel (chunked: gs_combine_kernel writes it)
                             if (P->out) {
                                 float* o = P->out + (size_t)item * 3;
                                 o[0] = 0.0f;
@@ -1655,10 +1664,11 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                             LI(L_SAMPLE) = P->round_base + ck * csz;
                             LI(L_BLEFT) = min(csz, P->ss.batch_size - ck * csz);
                         } else if (P->chunk) {
-                            // chunk sums: a coarse pixel's at item * cpp, a fine one's after
-                            // every coarse pixel's (the packed pixel and its queue position
-                            // share a tile, so both are in the fine region or neither)
-                            LI(L_ITEM) = fine ? P->fine_base + (item - P->fine_px) * cpp + ck : item * cpp + ck;
+                            // chunk sums, chunk-major: a coarse pixel's at ck * fine_px + item,
+                            // a fine one's after every coarse pixel's (the packed pixel and its
+                            // queue position share a tile, so both are in the fine region or neither)
+                            LI(L_ITEM) = fine ? P->fine_base + ck * (P->capacity - P->fine_px) + (item - P->fine_px)
+                                              : ck * P->fine_px + item;
                             LI(L_SAMPLE) = ck * csz;
                             LI(L_BLEFT) = min(csz, P->ss.batch_size - ck * csz);
                             if (ck == 0) atomicAdd(&s_cnt[C_PIX], 1ull);
@@ -2286,26 +2296,39 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 // (not a pageable hipMemcpyAsync, which can block the host until earlier work drains and
 // would need a host buffer that outlives the copy).
 __global__ void gs_params_kernel(KParams kp, KParams* __restrict__ dst) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) *dst = kp;
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        *dst = kp;
+        *kp.queue = 0u;  // (here rather than a memset: one stream operation fewer per frame)
+    }
 }
 
 // Chunked single-batch renders: a pixel's colour is the sum of its chunks' Σrgb, taken
 // in chunk (= sample) order, over the batch size (camera.rs:142-160 with one batch).
 // Padding slots of partial tiles get zeros.
+// Packed pixel k of this rank -> its image pixel (pi, pj); false for a padding slot (an empty
+// tile slot of the plan, or outside the image).
+__device__ __forceinline__ bool packed_pixel(const KParams* __restrict__ P, uint32_t k, uint32_t& pi, uint32_t& pj) {
+    const uint32_t tile_px = (uint32_t)(P->tile_w * P->tile_h);
+    const uint32_t slot = k / tile_px, w = k % tile_px;
+    const uint32_t pos = (uint32_t)P->rank + slot * (uint32_t)P->world_size;
+    const uint32_t tile = P->order ? (uint32_t)P->order[pos] : pos;  // -1: empty slot
+    if (tile == 0xFFFFFFFFu) return false;
+    pi = (tile % (uint32_t)P->tiles_x) * (uint32_t)P->tile_w + w % (uint32_t)P->tile_w;
+    pj = (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + w / (uint32_t)P->tile_w;
+    return pi < (uint32_t)P->cam.image_width && pj < (uint32_t)P->cam.image_height;
+}
+
 __global__ void gs_combine_kernel(const KParams* __restrict__ P) {
-    const uint32_t tile_px = (uint32_t)(P->tile_w * P->tile_h), cpp = P->cpp;
+    const uint32_t cpp = P->cpp;
     const double scount = 0.0 + (double)P->ss.batch_size;
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < P->capacity; k += gridDim.x * blockDim.x) {
-        const uint32_t slot = k / tile_px, w = k % tile_px;
-        const uint32_t pos = (uint32_t)P->rank + slot * (uint32_t)P->world_size;
-        const uint32_t tile = P->order ? (uint32_t)P->order[pos] : pos;  // -1: empty slot
-        const uint32_t pi = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu
-                                                : (tile % (uint32_t)P->tiles_x) * (uint32_t)P->tile_w + w % (uint32_t)P->tile_w;
-        const uint32_t pj = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu
-                                                : (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + w / (uint32_t)P->tile_w;
-        float* o = P->out ? P->out + (size_t)k * 3 : nullptr;
-        uint8_t* o8 = P->out8 ? P->out8 + (size_t)k * 3 : nullptr;
-        if (pi >= (uint32_t)P->cam.image_width || pj >= (uint32_t)P->cam.image_height) {
+        uint32_t pi = 0, pj = 0;
+        const bool real = packed_pixel(P, k, pi, pj);
+        const size_t oi = P->direct ? (size_t)pj * (uint32_t)P->cam.image_width + pi : (size_t)k;
+        float* o = P->out ? P->out + oi * 3 : nullptr;
+        uint8_t* o8 = P->out8 ? P->out8 + oi * 3 : nullptr;
+        if (!real) {
+            if (P->direct) continue;
             if (o) {
                 o[0] = 0.0f;
                 o[1] = 0.0f;
@@ -2320,12 +2343,14 @@ __global__ void gs_combine_kernel(const KParams* __restrict__ P) {
         }
         const bool fine = k >= P->fine_px;
         const uint32_t n = fine ? P->fine_cpp : cpp;
-        const double* p = P->partial + (fine ? (size_t)P->fine_base + (size_t)(k - P->fine_px) * n : (size_t)k * cpp) * 3;
+        // chunk-major sums: consecutive lanes read consecutive 24-B sums of each chunk
+        const size_t stride = (size_t)(fine ? P->capacity - P->fine_px : P->fine_px) * 3;
+        const double* p = P->partial + (fine ? (size_t)P->fine_base + (k - P->fine_px) : (size_t)k) * 3;
         double r = 0.0, g = 0.0, b = 0.0;
-        for (uint32_t c = 0; c < n; c++) {
-            r += p[c * 3];
-            g += p[c * 3 + 1];
-            b += p[c * 3 + 2];
+        for (uint32_t c = 0; c < n; c++, p += stride) {
+            r += p[0];
+            g += p[1];
+            b += p[2];
         }
         const double cr = r / scount, cg = g / scount, cb = b / scount;
         if (o) {
@@ -2354,22 +2379,15 @@ __global__ void gs_combine_kernel(const KParams* __restrict__ P) {
 // Before round 0: padding slots get their zero output; every real packed pixel enters the
 // first active list (one atomic per wave; the order inside a wave is kept).
 __global__ void gs_round_init_kernel(const KParams* __restrict__ P) {
-    const uint32_t tile_px = (uint32_t)(P->tile_w * P->tile_h);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t cap = P->capacity;
     const uint32_t span = (cap + 63u) & ~63u;  // whole waves take every iteration (ballots)
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < span; k += gridDim.x * blockDim.x) {
         bool real = false;
         if (k < cap) {
-            const uint32_t slot = k / tile_px, w = k % tile_px;
-            const uint32_t pos = (uint32_t)P->rank + slot * (uint32_t)P->world_size;
-            const uint32_t tile = P->order ? (uint32_t)P->order[pos] : pos;
-            if (tile != 0xFFFFFFFFu) {
-                const uint32_t pi = (tile % (uint32_t)P->tiles_x) * (uint32_t)P->tile_w + w % (uint32_t)P->tile_w;
-                const uint32_t pj = (tile / (uint32_t)P->tiles_x) * (uint32_t)P->tile_h + w / (uint32_t)P->tile_w;
-                real = pi < (uint32_t)P->cam.image_width && pj < (uint32_t)P->cam.image_height;
-            }
-            if (!real) {
+            uint32_t pi = 0, pj = 0;
+            real = packed_pixel(P, k, pi, pj);
+            if (!real && !P->direct) {
                 if (P->out) {
                     float* o = P->out + (size_t)k * 3;
                     o[0] = 0.0f;
@@ -2477,14 +2495,17 @@ __global__ void gs_round_combine_kernel(const KParams* __restrict__ P, uint32_t 
             if (!stop) stop = (uint32_t)sat_u64(scount, 4294967295.0, 4294967295ull) > P->ss.max_samples;
             if (stop) {
                 const double cr = r / scount, cg = g / scount, cb = b / scount;
+                uint32_t pi = 0, pj = 0;
+                if (P->direct) (void)packed_pixel(P, item, pi, pj);  // (an active pixel is real)
+                const size_t oi = P->direct ? (size_t)pj * (uint32_t)P->cam.image_width + pi : (size_t)item;
                 if (P->out) {
-                    float* o = P->out + (size_t)item * 3;
+                    float* o = P->out + oi * 3;
                     o[0] = (float)cr;
                     o[1] = (float)cg;
                     o[2] = (float)cb;
                 }
                 if (P->out8) {
-                    uint8_t* o8 = P->out8 + (size_t)item * 3;
+                    uint8_t* o8 = P->out8 + oi * 3;
                     o8[0] = color_byte(cr);
                     o8[1] = color_byte(cg);
                     o8[2] = color_byte(cb);
@@ -2524,6 +2545,8 @@ static std::atomic<int32_t> g_node_steps{0};  // 0: the scene's own (gs_device_s
 // 4632, 12 -> 4648-4651, 14 -> 4624, 16 -> 4592; GS_KIND_LEAF_BATCH for kind-batched kernels)
 static std::atomic<int32_t> g_leaf_batch{0};
 static std::atomic<int32_t> g_cam_batch{0};  // 0: the scene's own (gs_set_camera_batch)
+static std::atomic<int32_t> g_fine_chunk{0};  // guided tail (gs_debug_set_guided_tail): 0 = default
+static std::atomic<int32_t> g_tail_pct{0};
 #ifndef GS_KIND_SHADE_BATCH
 #define GS_KIND_SHADE_BATCH 44
 #endif
@@ -3113,6 +3136,13 @@ gs_status gs_debug_set_cube_lists(int32_t on) {
 
 gs_status gs_debug_set_partial_budget(uint64_t bytes) {
     g_partial_budget.store(bytes ? bytes : (4ull << 30));
+    return GS_OK;
+}
+
+gs_status gs_debug_set_guided_tail(int32_t fine_chunk, int32_t tail_pct) {
+    if (fine_chunk < 0 || tail_pct < 0) return fail(GS_ERR_ARG, "fine_chunk and tail_pct are >= 0 (0: the default)");
+    g_fine_chunk.store(fine_chunk);
+    g_tail_pct.store(tail_pct);
     return GS_OK;
 }
 
@@ -3741,22 +3771,23 @@ struct VisitArgs {
 };
 static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
                         const gs_partition* part, const gs_render_outputs* outs, gs_counters* d_counters, void* stream,
-                        hipEvent_t k_begin, hipEvent_t k_end, const VisitArgs* va);
+                        hipEvent_t k_begin, hipEvent_t k_end, const VisitArgs* va, bool direct = false);
 static gs_status ensure_placement(gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
                                   void* stream);
 
 gs_status gs_render_tiles_timed_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
                                       uint64_t seed, const gs_partition* part, const gs_render_outputs* outs,
-                                      gs_counters* d_counters, void* stream, hipEvent_t k_begin, hipEvent_t k_end) {
+                                      gs_counters* d_counters, void* stream, hipEvent_t k_begin, hipEvent_t k_end,
+                                      bool direct) {
     if (!ds || !cam) return fail(GS_ERR_ARG, "null argument");
     gs_status e = ensure_placement(const_cast<gs_device_scene*>(ds), cam, ss, stream);
     if (e != GS_OK) return e;
-    return launch(ds, cam, ss, seed, part, outs, d_counters, stream, k_begin, k_end, nullptr);
+    return launch(ds, cam, ss, seed, part, outs, d_counters, stream, k_begin, k_end, nullptr, direct);
 }
 
 static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
                         const gs_partition* part, const gs_render_outputs* outs, gs_counters* d_counters, void* stream,
-                        hipEvent_t k_begin, hipEvent_t k_end, const VisitArgs* va) {
+                        hipEvent_t k_begin, hipEvent_t k_end, const VisitArgs* va, bool direct) {
     if (!ds || !cam || !ss || !part || !outs || (!outs->rgb && !outs->rgb8)) return fail(GS_ERR_ARG, "null argument");
     if (!part_ok(cam, part)) return fail(GS_ERR_ARG, "bad partition / image size");
     if (ss->batch_size == 0) return fail(GS_ERR_ARG, "batch_size 0 never terminates (camera.rs:137)");
@@ -3792,7 +3823,9 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         if ((bs + c - 1) / c > 64u) c = (bs + 63u) / 64u;  // at most 64 chunks per pixel
         if (t_sample_chunk < 0)
             while (c < bs && (uint64_t)cap * ((bs + c - 1) / c) * 24u > t_partial_budget) c *= 2u;
-        if (t_sample_chunk < 0) {
+        const int32_t t_fc = g_fine_chunk.load(std::memory_order_relaxed);
+        const int32_t t_pct = g_tail_pct.load(std::memory_order_relaxed);
+        if (t_sample_chunk < 0 || t_pct > 0) {  // (an explicit chunk with a tail: gs_debug_set_guided_tail)
             // Guided tail: a work item of c samples started just before the queue runs dry
             // can keep its lane busy for c samples while every other lane idles, and a frame
             // with few items per lane ends on them (MI355X final_scene 400x400 x 64 spp,
@@ -3802,11 +3835,12 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
             // last coarse items finish.  Pixels with one chunk of all bs samples sum exactly
             // like the unsplit loop, fine pixels of 1-sample chunks too.
             c = std::min(c, bs);
-            const uint32_t fc = std::max<uint32_t>(1u, (bs + 63u) / 64u);
+            const uint32_t fc = std::max<uint32_t>(t_fc > 0 ? std::min<uint32_t>((uint32_t)t_fc, bs) : 1u,
+                                                   (bs + 63u) / 64u);  // (at most 64 chunks per pixel)
             const uint64_t tile_px = (uint64_t)part->tile_w * part->tile_h, slots = (uint64_t)cap / tile_px;
             const uint64_t lanes = (uint64_t)std::max(1, device_cus(dev)) * GS_BLOCK;
             if (fc < c && slots > 0) {
-                const uint64_t want = 2ull * lanes * c;  // samples
+                const uint64_t want = lanes * c * (uint64_t)(t_pct > 0 ? t_pct : 200) / 100u;  // samples
                 const uint64_t ft = std::min<uint64_t>(slots, (want + tile_px * bs - 1) / (tile_px * bs));
                 const uint32_t fpx = (uint32_t)((slots - ft) * tile_px), fcpp = (bs + fc - 1) / fc;
                 const uint64_t items = (uint64_t)fpx * ((bs + c - 1) / c) + ((uint64_t)cap - fpx) * fcpp;
@@ -3867,6 +3901,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     kp.claim = 1;  // set below, once the grid size is known
     kp.out = outs->rgb;
     kp.out8 = outs->rgb8;
+    kp.direct = direct ? 1u : 0u;
     kp.counters = (unsigned long long*)d_counters;
     kp.item_visits = outs->item_visits;
     kp.visits = va ? va->visits : nullptr;
@@ -4032,9 +4067,8 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     kp.queue = sl.queue;
     a.P = sl.params;
     if (outs->item_visits) HIPCHK(hipMemsetAsync(outs->item_visits, 0, (size_t)cap * sizeof(uint32_t), st));
-    hipLaunchKernelGGL(gs_params_kernel, dim3(1), dim3(64), 0, st, kp, sl.params);
+    hipLaunchKernelGGL(gs_params_kernel, dim3(1), dim3(64), 0, st, kp, sl.params);  // (zeroes the queue)
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemsetAsync(sl.queue, 0, 4, st));
     if (n_rounds) {
         // init (every real packed pixel active), then per round and segment: parameters,
         // the megakernel, the combine; all on the stream, no host synchronisation (a segment

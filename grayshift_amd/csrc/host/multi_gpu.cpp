@@ -130,6 +130,9 @@ struct Device {
     // render start / end, megakernel start / end, gather + unpack start / end
     hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     DBuf order, packed, packed8, cnt;
+    // the frame's counters, copied back on the stream behind the frame's last work, so the
+    // host's wait is the only synchronisation (a synchronous copy after it cost C1 ~25 us)
+    gs_counters* h_cnt = nullptr;  // pinned
 };
 
 #define HIPOK(x)                                                                                     \
@@ -191,6 +194,7 @@ struct gs_multi {
             d.packed.release();
             d.packed8.release();
             d.cnt.release();
+            if (d.h_cnt) (void)hipHostFree(d.h_cnt);
             if (d.scene) gs_device_scene_destroy(d.scene);
             if (d.stream) (void)hipStreamDestroy(d.stream);
         }
@@ -280,27 +284,32 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
     const int64_t W = cam->image_width, H = cam->image_height;
     have_rgb = have_rgb8 = false;
 
-    // Render: every device its own tiles, concurrently (launches are asynchronous).
-    for (int i = 0; i < n; i++) {
-        Device& d = dev[i];
-        HIPOK(hipSetDevice(d.id));
-        if (want_rgb) GROW(d.packed, cap * 12);
-        if (want8) GROW(d.packed8, cap * 3);
-        GROW(d.cnt, sizeof(gs_counters));
-        HIPOK(hipMemsetAsync(d.cnt.p, 0, sizeof(gs_counters), d.stream));
-        gs_partition p{i, n, tw, th, order.empty() ? nullptr : (const int32_t*)d.order.p, slots, 0};
-        gs_render_outputs o{want_rgb ? (float*)d.packed.p : nullptr, want8 ? (uint8_t*)d.packed8.p : nullptr,
-                            nullptr};
-        HIPOK(hipEventRecord(d.ev[0], d.stream));
-        s = gs_render_tiles_timed_async(d.scene, cam, ss, seed, &p, &o, (gs_counters*)d.cnt.p, d.stream, d.ev[2],
-                                        d.ev[3]);
-        if (s != GS_OK) return s;
-        HIPOK(hipEventRecord(d.ev[1], d.stream));
-    }
+    // One device and no collective: the render writes the frame itself (no packed tiles,
+    // no unpack: C1 saved the unpack kernel and a stream gap, ~20 us of a 0.9 ms frame).
+    const bool direct = n == 1 && comms.empty();
     Device& d0 = dev[0];
     HIPOK(hipSetDevice(d0.id));
     if (want_rgb) GROW(frame, W * H * 12);
     if (want8) GROW(frame8, W * H * 3);
+
+    // Render: every device its own tiles, concurrently (launches are asynchronous).
+    for (int i = 0; i < n; i++) {
+        Device& d = dev[i];
+        HIPOK(hipSetDevice(d.id));
+        if (want_rgb && !direct) GROW(d.packed, cap * 12);
+        if (want8 && !direct) GROW(d.packed8, cap * 3);
+        GROW(d.cnt, sizeof(gs_counters));
+        HIPOK(hipMemsetAsync(d.cnt.p, 0, sizeof(gs_counters), d.stream));
+        gs_partition p{i, n, tw, th, order.empty() ? nullptr : (const int32_t*)d.order.p, slots, 0};
+        gs_render_outputs o{want_rgb ? (float*)(direct ? frame.p : d.packed.p) : nullptr,
+                            want8 ? (uint8_t*)(direct ? frame8.p : d.packed8.p) : nullptr, nullptr};
+        HIPOK(hipEventRecord(d.ev[0], d.stream));
+        s = gs_render_tiles_timed_async(d.scene, cam, ss, seed, &p, &o, (gs_counters*)d.cnt.p, d.stream, d.ev[2],
+                                        d.ev[3], direct);
+        if (s != GS_OK) return s;
+        HIPOK(hipEventRecord(d.ev[1], d.stream));
+    }
+    HIPOK(hipSetDevice(d0.id));
     const void* src = want_rgb ? d0.packed.p : nullptr;
     const void* src8 = want8 ? d0.packed8.p : nullptr;
     if (!comms.empty()) {
@@ -331,15 +340,13 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
         HIPOK(hipSetDevice(d0.id));
         src = gathered.p;
         src8 = gathered8.p;
-    } else {
-        HIPOK(hipEventRecord(d0.ev[4], d0.stream));
-    }
+    }  // (no collective: the unpack is timed from the render's end event, ev[1])
     gs_partition pu{0, n, tw, th, order.empty() ? nullptr : (const int32_t*)d0.order.p, slots, 0};
-    if (want_rgb) {
+    if (want_rgb && !direct) {
         s = gs_unpack_tiles_part_async(cam, &pu, cap, src, frame.p, 12, d0.stream);
         if (s != GS_OK) return s;
     }
-    if (want8) {
+    if (want8 && !direct) {
         s = gs_unpack_tiles_part_async(cam, &pu, cap, src8, frame8.p, 3, d0.stream);
         if (s != GS_OK) return s;
     }
@@ -354,6 +361,10 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
         if (s != GS_OK) return s;
     }
     HIPOK(hipEventRecord(d0.ev[5], d0.stream));
+    for (auto& d : dev) {
+        HIPOK(hipSetDevice(d.id));
+        HIPOK(hipMemcpyAsync(d.h_cnt, d.cnt.p, sizeof(gs_counters), hipMemcpyDeviceToHost, d.stream));
+    }
     // Wait, then results.
     gs_counters total{};
     double rmax = 0.0, rmin = 1e300, kmax = 0.0, kmin = 1e300;
@@ -361,9 +372,7 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
         Device& d = dev[i];
         HIPOK(hipSetDevice(d.id));
         HIPOK(hipStreamSynchronize(d.stream));
-        gs_counters c{};
-        HIPOK(hipMemcpy(&c, d.cnt.p, sizeof(c), hipMemcpyDeviceToHost));
-        add_counters(total, c);
+        add_counters(total, *d.h_cnt);
         float ms = 0.0f, kms = 0.0f;
         HIPOK(hipEventElapsedTime(&ms, d.ev[0], d.ev[1]));
         HIPOK(hipEventElapsedTime(&kms, d.ev[2], d.ev[3]));
@@ -374,7 +383,7 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
     }
     HIPOK(hipSetDevice(d0.id));
     float gms = 0.0f;
-    HIPOK(hipEventElapsedTime(&gms, d0.ev[4], d0.ev[5]));
+    HIPOK(hipEventElapsedTime(&gms, comms.empty() ? d0.ev[1] : d0.ev[4], d0.ev[5]));
     have_rgb = want_rgb;
     have_rgb8 = want8;
     frame_w = cam->image_width;
@@ -455,6 +464,8 @@ gs_status gs_multi_create(const gs_flat_scene* scene, const gs_launch* launch, g
             return bail(fail(GS_ERR_HIP, "hipStreamCreateWithFlags failed"));
         for (auto& e : d.ev)
             if (hipEventCreate(&e) != hipSuccess) return bail(fail(GS_ERR_HIP, "hipEventCreate failed"));
+        if (hipHostMalloc((void**)&d.h_cnt, sizeof(gs_counters), hipHostMallocDefault) != hipSuccess)
+            return bail(fail(GS_ERR_OOM, "hipHostMalloc of the counters failed"));
     }
     if (collective) {  // one communicator rank per device, rank i = device i of the list
         m->comms.assign(n, nullptr);

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 9
+#define GS_ABI_VERSION 10
 
 typedef int32_t gs_status;
 enum {
@@ -291,6 +291,14 @@ gs_status gs_debug_set_cube_lists(int32_t on);
 /* Test hook: the auto sample-chunk rule's budget for chunk sums (default 4 GiB; 0
  * restores it).  A smaller budget makes renders take the chunk-doubling branch. */
 gs_status gs_debug_set_partial_budget(uint64_t bytes);
+
+/* Test hook (ABI 10): the auto sample-chunk rule's guided tail -- the samples per fine chunk
+ * (0: the default, batch_size / 64 rounded up, at least 1) and how much of the frame runs in
+ * fine chunks, as tail_pct percent of the device's lanes x the coarse chunk in samples (0:
+ * the default, 200).  tail_pct > 0 also gives an explicit gs_set_tuning sample_chunk (the
+ * coarse chunk) a tail.  Every choice renders the same samples; only the order in which a
+ * pixel's chunk sums are added changes. */
+gs_status gs_debug_set_guided_tail(int32_t fine_chunk, int32_t tail_pct);
 
 /* Upload a flattened scene to the current HIP device. */
 gs_status gs_device_scene_create(const gs_flat_scene* scene, gs_device_scene** out);

@@ -39,7 +39,7 @@ def test_every_declared_symbol_is_exported(built):
 
 
 def test_version_and_error_channel():
-    assert N.lib.gs_version() == N.GS_ABI_VERSION == 9
+    assert N.lib.gs_version() == N.GS_ABI_VERSION == 10
     assert N.lib.gs_set_tuning(-1, 0, 0, -1) == N.GS_ERR_ARG
     assert b"tuning" in N.lib.gs_last_error()
     assert N.lib.gs_set_tuning(65, 0, 0, -1) == N.GS_ERR_ARG

@@ -8,6 +8,7 @@
 #   configs every BASELINE config at its stated size, with parity and the CPU baseline, plus
 #           the adaptive A1 / A2 and final_scene at 1440^2 x 64 spp
 #   stamps  the stamps build's phase split and lane-efficiency summary of every config
+#   ranks   tools/rank_sim.py: every rank of 1/2/4/8-GPU planned frames of C4 and C5, alone
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
@@ -53,5 +54,12 @@ stamps)
     echo "== stamps $1"; cat $O/stamps_$1.txt
   done
   cp $R/profiles/stamps/*.json $R/gpurun_out/stamps_out/ ;;
+ranks)
+  # projection of the N-GPU frame from one GPU: every rank's planned share rendered alone
+  # (tools/rank_sim.py), C4 and C5 at their stated sizes
+  timeout -k 10 300 python3 -u $R/tools/rank_sim.py --config C4 --worlds 1,2,4,8 --all-ranks --plan > $O/rank_sim_C4.txt 2> $O/rank_sim_C4.err || { echo "rank_sim C4 failed"; tail -5 $O/rank_sim_C4.err; exit 1; }
+  grep projected $O/rank_sim_C4.txt
+  timeout -k 10 900 python3 -u $R/tools/rank_sim.py --config C5 --worlds 1,2,4,8 --all-ranks --plan --reps 1 > $O/rank_sim_C5.txt 2> $O/rank_sim_C5.err || { echo "rank_sim C5 failed"; tail -5 $O/rank_sim_C5.err; exit 1; }
+  grep projected $O/rank_sim_C5.txt ;;
 esac
 done

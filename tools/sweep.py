@@ -16,7 +16,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KNOBS = ["shade_batch", "leaf_batch", "sample_chunk", "blocks_per_cu", "tile", "node_steps", "camera_batch"]
+KNOBS = ["shade_batch", "leaf_batch", "sample_chunk", "blocks_per_cu", "tile", "node_steps", "camera_batch", "fine_chunk",
+         "tail_pct"]
 
 
 def main():
