@@ -189,6 +189,7 @@ struct KParams {
     // 1: out / out8 are the W x H frame itself (image pixel j * W + i), padding slots are not
     // written -- the one-device frame context, which then needs no unpack (round 5)
     uint32_t direct;
+    uint32_t zero_counters;  // 1: gs_params_kernel zeroes `counters` first (the frame context's own buffer)
     unsigned long long* counters;
     uint32_t* queue;
     uint32_t* item_visits;  // diagnostic: node visits per packed pixel (nullable)
@@ -2300,6 +2301,7 @@ __global__ void gs_params_kernel(KParams kp, KParams* __restrict__ dst) {
         *dst = kp;
         *kp.queue = 0u;  // (here rather than a memset: one stream operation fewer per frame)
     }
+    if (kp.zero_counters && blockIdx.x == 0 && threadIdx.x < sizeof(gs_counters) / 8) kp.counters[threadIdx.x] = 0ull;
 }
 
 // Chunked single-batch renders: a pixel's colour is the sum of its chunks' Σrgb, taken
@@ -3771,23 +3773,24 @@ struct VisitArgs {
 };
 static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
                         const gs_partition* part, const gs_render_outputs* outs, gs_counters* d_counters, void* stream,
-                        hipEvent_t k_begin, hipEvent_t k_end, const VisitArgs* va, bool direct = false);
+                        hipEvent_t k_begin, hipEvent_t k_end, const VisitArgs* va, bool direct = false,
+                        bool zero_counters = false);
 static gs_status ensure_placement(gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
                                   void* stream);
 
 gs_status gs_render_tiles_timed_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
                                       uint64_t seed, const gs_partition* part, const gs_render_outputs* outs,
                                       gs_counters* d_counters, void* stream, hipEvent_t k_begin, hipEvent_t k_end,
-                                      bool direct) {
+                                      bool direct, bool zero_counters) {
     if (!ds || !cam) return fail(GS_ERR_ARG, "null argument");
     gs_status e = ensure_placement(const_cast<gs_device_scene*>(ds), cam, ss, stream);
     if (e != GS_OK) return e;
-    return launch(ds, cam, ss, seed, part, outs, d_counters, stream, k_begin, k_end, nullptr, direct);
+    return launch(ds, cam, ss, seed, part, outs, d_counters, stream, k_begin, k_end, nullptr, direct, zero_counters);
 }
 
 static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss, uint64_t seed,
                         const gs_partition* part, const gs_render_outputs* outs, gs_counters* d_counters, void* stream,
-                        hipEvent_t k_begin, hipEvent_t k_end, const VisitArgs* va, bool direct) {
+                        hipEvent_t k_begin, hipEvent_t k_end, const VisitArgs* va, bool direct, bool zero_counters) {
     if (!ds || !cam || !ss || !part || !outs || (!outs->rgb && !outs->rgb8)) return fail(GS_ERR_ARG, "null argument");
     if (!part_ok(cam, part)) return fail(GS_ERR_ARG, "bad partition / image size");
     if (ss->batch_size == 0) return fail(GS_ERR_ARG, "batch_size 0 never terminates (camera.rs:137)");
@@ -3902,6 +3905,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     kp.out = outs->rgb;
     kp.out8 = outs->rgb8;
     kp.direct = direct ? 1u : 0u;
+    kp.zero_counters = zero_counters && d_counters ? 1u : 0u;
     kp.counters = (unsigned long long*)d_counters;
     kp.item_visits = outs->item_visits;
     kp.visits = va ? va->visits : nullptr;

@@ -11,11 +11,12 @@ extern "C" void gs_set_last_error(const char* msg);
 // recorded right before and after the megakernel itself, so the frame context can report
 // the dominant kernel's time apart from the parameter, queue and chunk-combine launches.
 // direct: outs->rgb / rgb8 are the W x H frame itself (image pixel j * W + i; padding slots
-// not written), so a one-device frame needs no unpack.
+// not written), so a one-device frame needs no unpack.  zero_counters: d_counters is set to
+// zero by the launch's first kernel instead of accumulated into (no memset before it).
 gs_status gs_render_tiles_timed_async(const gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss,
                                       uint64_t seed, const gs_partition* part, const gs_render_outputs* outs,
                                       gs_counters* d_counters, void* stream, hipEvent_t k_begin, hipEvent_t k_end,
-                                      bool direct = false);
+                                      bool direct = false, bool zero_counters = false);
 
 // The placement pilots still pending for a launch of `cam` / `ss` on n devices (scenes[i] on
 // devices[i], its stream streams[i]): every device's pilot is launched before any is waited

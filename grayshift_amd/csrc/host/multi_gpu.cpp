@@ -298,14 +298,13 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
         HIPOK(hipSetDevice(d.id));
         if (want_rgb && !direct) GROW(d.packed, cap * 12);
         if (want8 && !direct) GROW(d.packed8, cap * 3);
-        GROW(d.cnt, sizeof(gs_counters));
-        HIPOK(hipMemsetAsync(d.cnt.p, 0, sizeof(gs_counters), d.stream));
+        GROW(d.cnt, sizeof(gs_counters));  // (zeroed by the launch's parameter kernel)
         gs_partition p{i, n, tw, th, order.empty() ? nullptr : (const int32_t*)d.order.p, slots, 0};
         gs_render_outputs o{want_rgb ? (float*)(direct ? frame.p : d.packed.p) : nullptr,
                             want8 ? (uint8_t*)(direct ? frame8.p : d.packed8.p) : nullptr, nullptr};
         HIPOK(hipEventRecord(d.ev[0], d.stream));
         s = gs_render_tiles_timed_async(d.scene, cam, ss, seed, &p, &o, (gs_counters*)d.cnt.p, d.stream, d.ev[2],
-                                        d.ev[3], direct);
+                                        d.ev[3], direct, true);
         if (s != GS_OK) return s;
         HIPOK(hipEventRecord(d.ev[1], d.stream));
     }
@@ -360,7 +359,9 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
                                 (int64_t*)len.p, scratch.p, sb, d0.stream);
         if (s != GS_OK) return s;
     }
-    HIPOK(hipEventRecord(d0.ev[5], d0.stream));
+    // (direct without PPM text: nothing after the render to time, one stream marker fewer)
+    const bool timed_tail = !direct || (out && out->ppm_text);
+    if (timed_tail) HIPOK(hipEventRecord(d0.ev[5], d0.stream));
     for (auto& d : dev) {
         HIPOK(hipSetDevice(d.id));
         HIPOK(hipMemcpyAsync(d.h_cnt, d.cnt.p, sizeof(gs_counters), hipMemcpyDeviceToHost, d.stream));
@@ -383,7 +384,7 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
     }
     HIPOK(hipSetDevice(d0.id));
     float gms = 0.0f;
-    HIPOK(hipEventElapsedTime(&gms, comms.empty() ? d0.ev[1] : d0.ev[4], d0.ev[5]));
+    if (timed_tail) HIPOK(hipEventElapsedTime(&gms, comms.empty() ? d0.ev[1] : d0.ev[4], d0.ev[5]));
     have_rgb = want_rgb;
     have_rgb8 = want8;
     frame_w = cam->image_width;

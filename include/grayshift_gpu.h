@@ -340,7 +340,9 @@ typedef struct gs_stats {
     double total_ms;            /* host: the whole call */
     double render_ms_max;       /* slowest device's render: parameter + megakernel + chunk-combine launches */
     double render_ms_min;       /* fastest device's */
-    double gather_ms;           /* first device: RCCL gather (N > 1) + unpack (+ PPM text when asked) */
+    double gather_ms;           /* first device: RCCL gather (N > 1) + unpack (+ PPM text when asked);
+                                   one device without a collective renders into the frame itself:
+                                   the PPM text's time, else 0 (ABI 10) */
     uint64_t algorithmic_bytes; /* SURVEY.md §8d bytes of every launch (cache-served, not HBM) */
     uint64_t gathered_bytes;    /* bytes the gather delivered to the first device (0 for one device) */
     int32_t num_gpus;
