@@ -178,6 +178,17 @@ struct KParams {
     // capacity: no fine region).
     uint32_t fine_px, fine_base, fine_chunk, fine_cpp;
     uint32_t claim;  // work items a wave claims per queue atomic (its private reserve)
+#ifndef GS_CLAIM_DIV
+// claims per wave's share of the items (MI355X C1, 25 4-sample chunks per pixel: 8 -> 18 035-
+// 18 079, 4 -> 20 335, 2 -> 20 273 Msamples/s; C2, C4, A1, A2 within noise; the coarse
+// claims' cap of 32 binds for large frames either way: profiles/r05/ab_claim_div.txt)
+#define GS_CLAIM_DIV 4
+#endif
+#ifndef GS_CLAIM_FINE
+// the claim's cap for items of a few samples: one queue counter serialises the claims (MI355X
+// C1, 1-2 sample items: cap 32 -> 6786, 128 -> 12397, 512 -> 12559; perlin 3169, 3221, 2670)
+#define GS_CLAIM_FINE 128
+#endif
     uint32_t claim_fine;  // the same once the wave's claims reach the fine region
     // multiply-shift forms of the launch's fixed divisors (devmath.hpp UDiv): chunks per
     // pixel, tile pixels, 8x8 blocks per tile row, tile width, tiles per row, image width
@@ -2445,7 +2456,10 @@ __global__ void gs_round_params_kernel(KParams* __restrict__ P, uint32_t round, 
     P->n_items = n_seg * cpp;
     P->fine_base = 0xFFFFFFFFu;  // no fine region
     P->fine_px = P->capacity;
-    P->claim = max(1u, min(32u, P->n_items / max(1u, P->waves) / 8u));
+    // (items of a few samples claim more at a time, as fine chunks do: the one queue counter
+    // serialises the claims, and a tail round runs millions of 1-sample items)
+    P->claim = max(1u, min(whole || csz > 4u ? 32u : (uint32_t)GS_CLAIM_FINE,
+                           P->n_items / max(1u, P->waves) / (uint32_t)GS_CLAIM_DIV));
     P->claim_fine = P->claim;
     P->round_base = round * bs;
     P->seg_base = base;
@@ -3838,12 +3852,26 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
             // last coarse items finish.  Pixels with one chunk of all bs samples sum exactly
             // like the unsplit loop, fine pixels of 1-sample chunks too.
             c = std::min(c, bs);
-            const uint32_t fc = std::max<uint32_t>(t_fc > 0 ? std::min<uint32_t>((uint32_t)t_fc, bs) : 1u,
-                                                   (bs + 63u) / 64u);  // (at most 64 chunks per pixel)
             const uint64_t tile_px = (uint64_t)part->tile_w * part->tile_h, slots = (uint64_t)cap / tile_px;
             const uint64_t lanes = (uint64_t)std::max(1, device_cus(dev)) * GS_BLOCK;
+            // A small frame -- at most twice the default tail's samples -- of a scene whose
+            // samples are short and alike (no media, no BVHs under instances, no staged
+            // shading) runs wholly in fine chunks of 4 samples: there the items' fixed costs
+            // (claims, refills, chunk sums) outweigh the last chunk's length.  MI355X C1
+            // (400x225 x 100 spp, earth + sky): default tail of 2-sample chunks (21 of 28
+            // tiles) 14 727, 4-sample 16 579, every tile in 4-sample chunks 18 104 Msamples/s;
+            // 3, 5, 6 samples 15 977-17 205 (profiles/r05/sweep_C1_guided_tail*.txt).  Where
+            // samples vary (final_scene 400^2 x 64: every tile in 4-sample chunks 1 089, the
+            // 1-sample tail 1 381) and in larger frames (final_scene 1440^2 x 64: 1 sample
+            // 2 687, 4: 2 650) the tail keeps the finest chunks.
+            const bool simple = (ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_MIXED)) == 0;
+            const bool small = simple && (uint64_t)cap * bs <= 4ull * lanes * c && t_pct == 0;
+            const uint32_t fc_def = small ? std::min<uint32_t>(4u, c) : 1u;
+            const uint32_t fc = std::max<uint32_t>(t_fc > 0 ? std::min<uint32_t>((uint32_t)t_fc, bs) : fc_def,
+                                                   (bs + 63u) / 64u);  // (at most 64 chunks per pixel)
             if (fc < c && slots > 0) {
-                const uint64_t want = lanes * c * (uint64_t)(t_pct > 0 ? t_pct : 200) / 100u;  // samples
+                const uint64_t want = small ? (uint64_t)cap * bs  // (every tile)
+                                            : lanes * c * (uint64_t)(t_pct > 0 ? t_pct : 200) / 100u;  // samples
                 const uint64_t ft = std::min<uint64_t>(slots, (want + tile_px * bs - 1) / (tile_px * bs));
                 const uint32_t fpx = (uint32_t)((slots - ft) * tile_px), fcpp = (bs + fc - 1) / fc;
                 const uint64_t items = (uint64_t)fpx * ((bs + c - 1) / c) + ((uint64_t)cap - fpx) * fcpp;
@@ -3986,15 +4014,12 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     const uint64_t waves = (uint64_t)blocks * (GS_BLOCK / 64);
     kp.waves = (uint32_t)waves;
     kp.lanes = (uint32_t)(blocks * GS_BLOCK);
-    kp.claim = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, (uint64_t)kp.n_items / waves / 8));
-#ifndef GS_CLAIM_FINE
-#define GS_CLAIM_FINE 128  // MI355X C1 (1-2 sample items): 32 -> 6786, 128 -> 12397, 512 -> 12559; perlin 3169, 3221, 2670
-#endif
-    kp.claim_fine = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(GS_CLAIM_FINE, (uint64_t)kp.n_items / waves / 8));
+    kp.claim = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, (uint64_t)kp.n_items / waves / GS_CLAIM_DIV));
+    kp.claim_fine = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(GS_CLAIM_FINE, (uint64_t)kp.n_items / waves / GS_CLAIM_DIV));
     // The u32 queue counter runs past n_items by at most one claim per wave (each wave's
     // last, failed claim): it must not wrap.
     if ((uint64_t)std::max<uint64_t>(kp.n_items, (uint64_t)seg_px * ss->batch_size) +
-            (uint64_t)std::max<uint32_t>(32, std::max(kp.claim, kp.claim_fine)) * (waves + 1) >= 0xFFFFFFFFull)
+            (uint64_t)std::max<uint32_t>(GS_CLAIM_FINE, std::max(kp.claim, kp.claim_fine)) * (waves + 1) >= 0xFFFFFFFFull)
         return fail(GS_ERR_ARG, "too many work items for the 32-bit work queue");
 
     // This launch's slot.  A slot whose last launch ran on this very stream is reused first:

@@ -29,7 +29,10 @@ bench)
   find $O/stats -name "*kernel_stats.csv" -exec head -6 {} \; ;;
 pmc)
   for c in ${PMC_CONFIGS:-C4 C3 C5 A2 final_scene}; do
-    if [ $c = final_scene ]; then BA="--width 1440 --spp 64"; PT=final_scene_w1440_s64; else BA=""; PT=$c; fi
+    case $c in
+      final_scene|cornell_smoke) BA="--width 1440 --spp 64"; PT=${c}_w1440_s64 ;;
+      *) BA=""; PT=$c ;;
+    esac
     CONFIG=$c BENCH_ARGS="$BA" PMC_TAG=$PT bash $R/tools/pmc.sh || exit 1
   done
   # (later stages' bench lines read them from the tree; gpurun_out/pmc_out comes back to commit)
