@@ -2949,6 +2949,16 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
     // most GS_NESTED_STACK (the device walk is threaded and needs no stack; the bound keeps
     // the host's threading finite).  Subtrees may be shared between chains (instancing);
     // the depth bound ends cycles and a visit budget ends blow-ups.
+    // A ConstantMedium: its boundary a primitive or list behind an optional chain.
+    auto medium_ok = [&](uint32_t cur) -> int {
+        uint32_t i = cur & GS_REF_MASK;
+        if (i >= s.n_media || !s.media) return 1;
+        if (s.media[i].material >= s.n_materials) return 1;
+        uint32_t b = s.media[i].boundary;
+        const int e = chain_ok(b, 2);
+        if (e) return e;
+        return shape_ok(b);
+    };
     bool nested = false;
     uint64_t nested_budget = 64ull << 20;
     auto nested_ok = [&](uint32_t root) -> int {
@@ -2965,7 +2975,9 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
                 st.push_back({s.nodes[i].left, d + 1});
                 if (s.nodes[i].right != GS_REF_NONE) st.push_back({s.nodes[i].right, d + 1});
             } else {
-                const int e = shape_ok(r);
+                // (since round 5 the tree is walked by the main passes, whose leaf test takes
+                // media like the top level's: the hit's instance is the tree's chain)
+                const int e = (r >> GS_REF_SHIFT) == GS_REF_MEDIUM ? medium_ok(r) : shape_ok(r);
                 if (e) return e;
             }
         }
@@ -2977,15 +2989,7 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
         int e = chain_ok(cur);
         if (e) return e;
         if ((cur >> GS_REF_SHIFT) == GS_REF_NODE && cur != r) return nested_ok(cur);
-        if ((cur >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
-            uint32_t i = cur & GS_REF_MASK;
-            if (i >= s.n_media || !s.media) return 1;
-            if (s.media[i].material >= s.n_materials) return 1;
-            uint32_t b = s.media[i].boundary;
-            e = chain_ok(b, 2);
-            if (e) return e;
-            return shape_ok(b);
-        }
+        if ((cur >> GS_REF_SHIFT) == GS_REF_MEDIUM) return medium_ok(cur);
         if ((cur >> GS_REF_SHIFT) == GS_REF_NODE) return cur != r ? 2 : 1;
         return shape_ok(cur);
     };
@@ -3010,9 +3014,9 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
             int e = leaf_ok(r);
             if (e == 1) return bad("leaf reference");
             if (e == 2) return unsup("instance chain deeper than 4, a BVH under an instance deeper than " +
-                                     std::to_string(GS_NESTED_STACK) + " or with leaves that are not lists or "
-                                     "primitives, a BVH inside a medium boundary, nested media, or a list member "
-                                     "that is not a primitive");
+                                     std::to_string(GS_NESTED_STACK) + " or with leaves that are not lists, "
+                                     "primitives or media, a BVH inside a medium boundary, nested media, or a list "
+                                     "member that is not a primitive");
         }
     }
     *depth_out = maxd;

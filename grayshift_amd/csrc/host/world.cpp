@@ -407,8 +407,8 @@ uint32_t BVHNode::flatten(Flattener& f) const {
 uint32_t ConstantMedium::flatten(Flattener& f) const {  // volume.rs:10-29
     if (f.inside_medium)
         throw std::domain_error("ConstantMedium inside a ConstantMedium boundary is not supported on the device path");
-    if (f.inside_nested_bvh)
-        throw std::domain_error("ConstantMedium inside a BVH under Translate/RotateY is not supported on the device path");
+    // (inside a BVH under Translate/RotateY: supported since round 5, the device walks such
+    // trees in its main passes and tests their media like the top level's)
     size_t idx = f.media.size();
     check_index(idx, "media");
     f.media.push_back(gs_medium{});

@@ -278,7 +278,8 @@ public:
 };
 
 // hittable/volume.rs:10-68.  The boundary is any Hittable but a BVH or another medium
-// on the device path (flatten throws std::domain_error otherwise).
+// on the device path (flatten throws std::domain_error otherwise); the medium itself may sit
+// in a BVH under Translate/RotateY (round 5).
 class ConstantMedium : public Hittable {
 public:
     ConstantMedium(HittablePtr boundary, double density, MaterialPtr phase_function)

@@ -67,3 +67,30 @@ def test_media_partition_invariance():
     full, fc = g.render(sc, seed=2)
     part, pc = _render_partitioned(sc, 3, 16, seed=2)
     assert np.array_equal(full, part) and fc == pc
+
+
+@pytest.mark.parametrize("phase", ["isotropic", "lambertian"])
+def test_media_inside_a_bvh_under_instances_match_oracle(phase):
+    """ConstantMedium leaves inside a BVH under Translate(RotateY(...)) (volume.rs:10-68 in a
+    BVHNode, hittable.rs:107-211 around it): accepted since round 5, when the device began
+    walking such trees in its main node and leaf passes, where a medium leaf is tested as at
+    the top level and its hit carries the tree's chain.  Frames and counters against the
+    oracle; the media draw inside traversal, so this also pins the walk's visit order."""
+    b = g.SceneBuilder()
+    glass = b.dielectric(1.5)
+    fog = b.lambertian((0.2, 0.4, 0.9)) if phase == "lambertian" else b.isotropic((0.2, 0.4, 0.9))
+    white = b.lambertian((0.73, 0.73, 0.73))
+    items = [b.sphere((0.3 * k - 1.2, 0.25 * (k % 3), 0.0), 0.12, white) for k in range(9)]
+    items.append(b.medium(b.sphere((0.0, 0.2, 0.0), 0.8, glass), 1.2, fog))
+    items.append(b.medium(b.cube((0.6, -0.4, -0.4), (1.2, 0.3, 0.4), white), 2.0, b.isotropic((0.9, 0.8, 0.7))))
+    b.add(b.translate(b.rotate_y(b.bvh(items), 25.0), (0.2, 0.1, -0.3)))
+    b.add(b.sphere((0.0, -101.0, 0.0), 100.0, b.lambertian((0.5, 0.5, 0.5))))
+    b.add(b.quad((-2.0, 3.0, -2.0), (4.0, 0.0, 0.0), (0.0, 0.0, 4.0), b.diffuse_light((4.0, 4.0, 4.0))))
+    b.background_solid((0.3, 0.4, 0.5))
+    cam = camera_spec(1.0, 40, 20, 40.0, (0.0, 1.0, 6.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 0.0, 6.0)
+    sc = scenes.Scene("nested_fog", b.build(), cam, fixed_spp(16))
+    out, gc = g.render(sc, seed=9)
+    ref, rc = oracle.render(sc, seed=9)
+    assert maxdiff(out, ref) < TOL
+    assert counters_match(gc, rc)
+    assert gc["medium_tests"] > 0 and gc["instance_tests"] > 0
