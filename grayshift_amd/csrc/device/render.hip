@@ -2444,8 +2444,15 @@ __global__ void gs_round_params_kernel(KParams* __restrict__ P, uint32_t round, 
     if (chunk_req > 0) {
         csz = min((uint32_t)chunk_req, bs);
     } else {
+#ifndef GS_ROUND_CSZ_MIN
+#define GS_ROUND_CSZ_MIN 1u  // (A/B: the smallest sample chunk of a round's items)
+#endif
+#ifndef GS_ROUND_ITEMS_PER_LANE
+#define GS_ROUND_ITEMS_PER_LANE 8ull
+#endif
         csz = min(16u, bs);
-        while (csz > 1u && (uint64_t)n_seg * ((bs + csz - 1u) / csz) < 8ull * P->lanes) csz >>= 1;
+        while (csz > GS_ROUND_CSZ_MIN && (uint64_t)n_seg * ((bs + csz - 1u) / csz) < GS_ROUND_ITEMS_PER_LANE * P->lanes)
+            csz >>= 1;
     }
     const uint32_t cpp = whole ? 1u : (bs + csz - 1u) / csz;
     P->per_sample = whole ? 0u : 1u;
