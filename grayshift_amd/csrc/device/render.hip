@@ -65,8 +65,6 @@ using namespace gsd;
 #ifndef GS_ROUND_WHOLE_MAX_BATCH
 #define GS_ROUND_WHOLE_MAX_BATCH 256
 #endif
-// The nested trees' records (BVHs under instances) mirrored in LDS after the quads, placed
-// shallowest first (0: read from global memory only)
 #define GS_NESTED_STACK 32  // max depth of a BVH under a Translate/RotateY chain (a validation bound; the walk is stackless)
 // Kernel feature flags (template argument): scenes without them compile the code out.
 #define GS_FEAT_MEDIA 1   // ConstantMedium leaves (RNG draws inside traversal)
@@ -258,10 +256,10 @@ struct KArgs {
 // by the shade pass for a finished sample; one advance() at the loop head serves both).
 enum { S_NEED = 0, S_TRACE = 1, S_SHADE = 2, S_DONE = 3, S_CAM = 4 };
 
-// Device-side refs in the two-child node records of BVHs under instances (nested_bvh):
-// a BVH node is its bare index (< 2^26), leaves keep their ABI tag (kind >= 2 in the top
-// 4 bits), and "none" is all ones.  So `cur >= DREF_LEAF` tells a leaf in one compare and
-// a node's byte offset is `cur << 6`.  (Leaf, list and instance records keep ABI refs.)
+// DevScene::root in the two-child records' terms: a BVH node is its bare index (< 2^26),
+// leaves keep their ABI tag (kind >= 2 in the top 4 bits), "none" is all ones.  (The
+// kernels start at KArgs::root, the threaded tree's first link; this form is kept for the
+// scene record only.)
 #define DREF_NONE 0xFFFFFFFFu
 #define DREF_LEAF (1u << GS_REF_SHIFT)
 __host__ __device__ inline uint32_t device_ref(uint32_t abi_ref) {
