@@ -47,6 +47,12 @@ def test_version_and_error_channel():
     assert N.lib.gs_set_tuning(60, 0, 8, -2) == N.GS_ERR_ARG
     assert N.lib.gs_set_tuning(60, 0, 8, -1) == N.GS_OK
     assert N.lib.gs_set_tuning(0, 0, 0, -1) == N.GS_OK  # (0: the scene's own shade batch, ABI 8)
+    # the guided tail's test hook (ABI 10): 0 = the defaults, negative values rejected
+    assert N.lib.gs_debug_set_guided_tail(-1, 0) == N.GS_ERR_ARG
+    assert N.lib.gs_debug_set_guided_tail(0, -5) == N.GS_ERR_ARG
+    assert b"fine_chunk" in N.lib.gs_last_error()
+    assert N.lib.gs_debug_set_guided_tail(4, 300) == N.GS_OK
+    assert N.lib.gs_debug_set_guided_tail(0, 0) == N.GS_OK
 
 
 @pytest.mark.parametrize("name", ["gs_object", "gs_material_spec", "gs_texture_spec", "gs_image_spec",
