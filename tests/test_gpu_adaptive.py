@@ -159,3 +159,29 @@ def test_round_items_at_a_chip_filling_size(items):
         auto, cauto = g.render(sc, seed=9)
     assert np.array_equal(a, ref) and ca == rc
     assert np.array_equal(auto, ref) and cauto == rc
+
+
+def test_rounds_past_every_pixels_stop_are_empty_and_cheap():
+    """settings whose pixels all stop after the first batch while max_samples
+    allows hundreds of rounds (here 257 rounds of 4 samples).  Every round after the first
+    has no active pixel, so its launches must return at once (render.hip: the megakernel's
+    early return on an empty round, before the LDS mirror copy) -- and the frame is still
+    the per-lane loop's, bit for bit, and the oracle's."""
+    b = g.SceneBuilder()
+    b.add(b.sphere((0, 0, 60), 1.0, b.lambertian((0.5, 0.5, 0.5))))  # behind the camera
+    b.background_solid((0.7, 0.8, 1.0))
+    cam = camera_spec(1.0, 48, 50, 20.0, (0, 0, 30), (0, 0, 0), (0, 1, 0), 0.0, 30.0)
+    # every primary ray sees the solid sky: every sample of a pixel is the same colour, so
+    # the variance is 0 and the first stop test passes (0 < mean^2 * tol^2)
+    sc = scenes.Scene("sky", b.build(), cam, sample_settings(0.95, 0.05, 4, 1024))
+    with _mode(2):
+        st = {}
+        a, ca = g.render(sc, seed=4, stats=st)
+    with _mode(0):
+        ref_loop, cl = g.render(sc, seed=4)
+    assert np.array_equal(a, ref_loop) and ca == cl
+    assert ca["paths"] == 48 * 48 * 4  # one batch per pixel
+    ref, rc = oracle.render(sc, seed=4)
+    assert float(np.abs(a.astype(np.float64) - ref.astype(np.float64)).max()) < TOL
+    # 257 rounds x (parameters + megakernel + combine), 256 of them empty: launch overhead
+    assert st["kernel_ms_max"] < 100.0, st
