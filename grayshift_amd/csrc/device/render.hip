@@ -2683,6 +2683,10 @@ struct gs_device_scene {
     int32_t leaf_batch = 12;                 // lanes at a leaf before a leaf pass (scene's choice)
     int32_t shade_batch = 52;                // finished lanes a wave shades together (scene's choice)
     int32_t cam_batch = 1;                   // lanes waiting for camera rays before a wave runs get_ray
+    // A sample's cost on this device, lane-microseconds (kernel time x lanes / samples), from
+    // the frame context's last frame (gs_device_scene_note_frame); 0 = not measured yet.  The
+    // guided tail's small-frame rule reads it (launch).
+    std::atomic<double> lane_us_per_sample{0.0};
     uint32_t node_records = 0, leaf_records = 0;
     double nodes_per_leaf = 0.0, other_leaf_frac = 0.0;
     // Launch state, mutated by launches of a const scene: guarded by `mu`.
@@ -3700,6 +3704,9 @@ gs_status gs_device_scene_destroy(gs_device_scene* ds) {
     return GS_OK;
 }
 
+#ifndef GS_SHORT_SAMPLE_LANE_US
+#define GS_SHORT_SAMPLE_LANE_US 50.0
+#endif
 // Compute units of a device (cached: the attribute query costs ~0.5 ms).
 static int device_cus(int dev) {
     static std::atomic<int> cache[64];
@@ -3710,6 +3717,12 @@ static int device_cus(int dev) {
         cache[dev].store(v, std::memory_order_relaxed);
     }
     return v;
+}
+
+void gs_device_scene_note_frame(gs_device_scene* ds, double kernel_ms, uint64_t samples) {
+    if (!ds || !(kernel_ms > 0.0) || samples == 0) return;
+    const double lanes = (double)device_cus(ds->device) * GS_BLOCK;
+    ds->lane_us_per_sample.store(kernel_ms * 1e3 * lanes / (double)samples, std::memory_order_relaxed);
 }
 
 static bool part_ok(const gs_camera* cam, const gs_partition* p) {
@@ -3873,8 +3886,17 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
             // samples vary (final_scene 400^2 x 64: every tile in 4-sample chunks 1 089, the
             // 1-sample tail 1 381) and in larger frames (final_scene 1440^2 x 64: 1 sample
             // 2 687, 4: 2 650) the tail keeps the finest chunks.
+            // Once a frame of the scene has been timed (the frame context), the rule also needs
+            // short samples: at most GS_SHORT_SAMPLE_LANE_US lane-microseconds each.  400-px
+            // reference scenes, rule on / off (profiles/r05/small_frame_rule_scenes.txt),
+            // Msamples/s: earth 17 317 / 8 725, hdri 13 956 / 7 100, triangles 14 582 / 8 465,
+            // quads 13 402 / 11 088 (17-34 lane-us a sample) -- but checkered_spheres 10 523 /
+            // 14 047, cornell_box 8 272 / 8 918, perlin_spheres 1 524 / 3 320, simple_light
+            // 1 056 / 2 762 (77-391 lane-us: their last 4-sample items drag the frame).
             const bool simple = (ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_MIXED)) == 0;
-            const bool small = simple && (uint64_t)cap * bs <= 4ull * lanes * c && t_pct == 0;
+            const double lus = ds->lane_us_per_sample.load(std::memory_order_relaxed);
+            const bool short_samples = lus == 0.0 || lus <= GS_SHORT_SAMPLE_LANE_US;
+            const bool small = simple && short_samples && (uint64_t)cap * bs <= 4ull * lanes * c && t_pct == 0;
             const uint32_t fc_def = small ? std::min<uint32_t>(4u, c) : 1u;
             const uint32_t fc = std::max<uint32_t>(t_fc > 0 ? std::min<uint32_t>((uint32_t)t_fc, bs) : fc_def,
                                                    (bs + 63u) / 64u);  // (at most 64 chunks per pixel)

@@ -24,3 +24,7 @@ gs_status gs_render_tiles_timed_async(const gs_device_scene* ds, const gs_camera
 // any pilot ran.  Leaves the current device changed.
 gs_status gs_placement_prepare(gs_device_scene* const* scenes, const int* devices, void* const* streams, int n,
                                const gs_camera* cam, const gs_sample_settings* ss, int* ran);
+
+// A timed frame of the scene on its device: its megakernel time and samples (paths), which
+// set the scene's per-sample cost that the guided tail's small-frame rule reads (render.hip).
+extern "C" void gs_device_scene_note_frame(gs_device_scene* ds, double kernel_ms, uint64_t samples);

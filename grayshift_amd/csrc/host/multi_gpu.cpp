@@ -377,6 +377,7 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
         float ms = 0.0f, kms = 0.0f;
         HIPOK(hipEventElapsedTime(&ms, d.ev[0], d.ev[1]));
         HIPOK(hipEventElapsedTime(&kms, d.ev[2], d.ev[3]));
+        gs_device_scene_note_frame(d.scene, (double)kms, d.h_cnt->paths);
         rmax = std::max(rmax, (double)ms);
         rmin = std::min(rmin, (double)ms);
         kmax = std::max(kmax, (double)kms);
