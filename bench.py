@@ -180,14 +180,18 @@ def main_context(a):
     for _ in range(a.warmup):
         m.render(seed=a.seed)
     sync_all()
-    kms, tot = [], None
+    # every frame's gs_stats into its own preallocated struct; read after the timed loop
+    stats = [N.gs_stats() for _ in range(a.steps)]
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        r = m.render(seed=a.seed)  # synchronous: returns once the frame is unpacked
-        kms.append(r["stats"]["kernel_ms_max"])
-        tot = r["counters"] if tot is None else {k: tot[k] + v for k, v in r["counters"].items()}
+    for st in stats:
+        m.render_stats(a.seed, st)  # synchronous: returns once the frame is in the device frame
     sync_all()
     elapsed = time.perf_counter() - t0
+    kms = [st.kernel_ms_max for st in stats]
+    tot = None
+    for st in stats:
+        cd = st.counters.as_dict()
+        tot = cd if tot is None else {k: tot[k] + v for k, v in cd.items()}
     c = {k: v // a.steps for k, v in tot.items()}
     d_rgb, dev0 = m.frame_ptr()
     img = np.zeros((m.height, m.width, 3), dtype=np.float32)

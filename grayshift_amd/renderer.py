@@ -145,6 +145,13 @@ class MultiRenderer:
         res["stats"] = {k: v for k, v in st.as_dict().items() if k != "counters"}
         return res
 
+    def render_stats(self, seed, st):
+        """One frame, the frame left on the first device, its gs_stats written into `st` (a
+        caller-owned N.gs_stats) -- render() without the per-call Python conversions, for
+        timed loops (bench.py)."""
+        N.check(N.lib.gs_multi_render(self.handle, C.byref(self.cam), C.byref(self.settings), seed, None,
+                                      C.byref(st)))
+
     def scene_info(self, rank=0):
         """gs_device_scene_info of the scene on rank `rank`'s device."""
         d = C.c_void_p()
