@@ -29,6 +29,29 @@ def test_committed_pmc_summary_matches_the_built_code_object(built):
     assert os.path.exists(path), "no PMC summary for code object %s: run tools/pmc.sh and commit it" % h
 
 
+def test_every_config_line_can_carry_its_fractions(built):
+    """every BASELINE config's bench line carries the measured VALU-busy
+    fraction (PMC summary) and the lane efficiency (stamps summary) of the code object it
+    times -- both committed for the built library's hash, and bench.py's roofline reads them
+    into frac, lane_frac and useful_frac = frac x lane_frac.  No device needed: the roofline
+    is assembled from the committed files and a counter set of the right shape."""
+    import argparse
+    import json
+    import bench
+    h = codeobj.code_object_hash(LIB_PATH)
+    for cfg in ["C1", "C2", "C3", "C4", "C5", "A1", "A2", "final_scene_w1440_s64", "cornell_smoke_w1440_s64"]:
+        for kind in ("pmc", "stamps"):
+            path = os.path.join(ROOT, "profiles", kind, "%s_%s.json" % (cfg, h))
+            assert os.path.exists(path), "no %s summary of %s for code object %s" % (kind, cfg, h)
+    line = json.loads(open(os.path.join(ROOT, "profiles", "r05", "final_configs.jsonl")).readline())
+    a = argparse.Namespace(config="C4", width=None, spp=None, pmc_dir=os.path.join(ROOT, "profiles", "pmc"))
+    r = bench.roofline(a, {k: 0 for k in bench.BYTES}, 1, 354.6, False)
+    lane = json.load(open(os.path.join(ROOT, "profiles", "stamps", "C4_%s.json" % h)))["lane_frac"]
+    assert r["code_object"] == h and r["frac"] is not None and r["lane_frac"] == lane
+    assert abs(r["useful_frac"] - r["frac"] * lane) < 1e-4
+    assert line["roofline"]["code_object"] == h  # the committed configs were measured on this code
+
+
 def test_product_kernels_have_no_scratch(built):
     """Every kernel the product launches for a render runs without private (scratch)
     memory: register spills in the megakernel cost a memory round trip inside the loop
