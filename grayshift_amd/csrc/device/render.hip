@@ -1903,7 +1903,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     for (int nstep = 0; nstep < A.node_steps; nstep++) node_step(slow_t{}, mixed_t{});
                 }
                 GS_MARK("node_end");
-            } else if (kNested && __builtin_amdgcn_ballot_w64(cur == THR_RET) != 0) {
+#ifndef GS_NESTED_RET_MERGE
+#define GS_NESTED_RET_MERGE 0  // (A/B: take returns at the start of the leaf pass, no pass of their own)
+#endif
+            } else if (kNested && !GS_NESTED_RET_MERGE && __builtin_amdgcn_ballot_w64(cur == THR_RET) != 0) {
                 // Return passes (GS_FEAT_NESTED): a lane whose walk of a BVH under an instance
                 // chain ended (the tree's last links are THR_RET) takes back its top-level ray
                 // and goes on at the record after the instance's leaf -- where BVHNode::hit's
@@ -1916,6 +1919,16 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     LNINST = GS_REF_NONE;
                 }
             } else if (at_leaf) {
+                if constexpr (kNested && GS_NESTED_RET_MERGE) {
+                    if (cur == THR_RET) {
+                        const double* sv = P->nest_save + ((size_t)blockIdx.x * GS_BLOCK + tid) * 8u;
+                        ray.o = mk(sv[0], sv[1], sv[2]);
+                        ray.d = mk(sv[3], sv[4], sv[5]);
+                        cur = (uint32_t)__double_as_longlong(sv[6]);
+                        LNINST = GS_REF_NONE;
+                    }
+                }
+                if (!(kNested && GS_NESTED_RET_MERGE) || cur > THR_END) {
                 GS_MARK("leaf_begin");
                 double scx, scy, scz, sr;
                 uint32_t next, ref;
@@ -2118,6 +2131,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 }
                 }  // take_leaf
                 GS_MARK("leaf_end");
+                }  // (GS_NESTED_RET_MERGE: a returned lane's next record is a leaf)
             }
             // Nested-BVH kernels and media kernels with sphere leaf runs: the certified test's
             // ray constants are recomputed after a leaf pass (the same function of the same
