@@ -104,7 +104,9 @@ typedef struct gs_list {
 } gs_list;
 
 /* Instance transform, one per Translate / RotateY (hittable.rs:93-215). 32 B.
- * child: the wrapped object (another instance, a list or a primitive). */
+ * child: the wrapped object (another instance, a list, a primitive, a medium, or a BVH node:
+ * a BVH under an instance chain, whose leaves are lists, primitives or media -- not
+ * instances; at most 4 instances in a chain).  Other compositions: GS_ERR_UNSUPPORTED. */
 enum { GS_INST_TRANSLATE = 1, GS_INST_ROTATE_Y = 2 };
 typedef struct gs_instance {
     uint32_t kind;
