@@ -1903,10 +1903,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     for (int nstep = 0; nstep < A.node_steps; nstep++) node_step(slow_t{}, mixed_t{});
                 }
                 GS_MARK("node_end");
-#ifndef GS_NESTED_RET_MERGE
-#define GS_NESTED_RET_MERGE 0  // (A/B: take returns at the start of the leaf pass, no pass of their own)
-#endif
-            } else if (kNested && !GS_NESTED_RET_MERGE && __builtin_amdgcn_ballot_w64(cur == THR_RET) != 0) {
+            } else if (kNested && __builtin_amdgcn_ballot_w64(cur == THR_RET) != 0) {
                 // Return passes (GS_FEAT_NESTED): a lane whose walk of a BVH under an instance
                 // chain ended (the tree's last links are THR_RET) takes back its top-level ray
                 // and goes on at the record after the instance's leaf -- where BVHNode::hit's
@@ -1919,16 +1916,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     LNINST = GS_REF_NONE;
                 }
             } else if (at_leaf) {
-                if constexpr (kNested && GS_NESTED_RET_MERGE) {
-                    if (cur == THR_RET) {
-                        const double* sv = P->nest_save + ((size_t)blockIdx.x * GS_BLOCK + tid) * 8u;
-                        ray.o = mk(sv[0], sv[1], sv[2]);
-                        ray.d = mk(sv[3], sv[4], sv[5]);
-                        cur = (uint32_t)__double_as_longlong(sv[6]);
-                        LNINST = GS_REF_NONE;
-                    }
-                }
-                if (!(kNested && GS_NESTED_RET_MERGE) || cur > THR_END) {
                 GS_MARK("leaf_begin");
                 double scx, scy, scz, sr;
                 uint32_t next, ref;
@@ -2131,7 +2118,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 }
                 }  // take_leaf
                 GS_MARK("leaf_end");
-                }  // (GS_NESTED_RET_MERGE: a returned lane's next record is a leaf)
             }
             // Nested-BVH kernels and media kernels with sphere leaf runs: the certified test's
             // ray constants are recomputed after a leaf pass (the same function of the same
@@ -2456,15 +2442,10 @@ __global__ void gs_round_params_kernel(KParams* __restrict__ P, uint32_t round, 
     if (chunk_req > 0) {
         csz = min((uint32_t)chunk_req, bs);
     } else {
-#ifndef GS_ROUND_CSZ_MIN
-#define GS_ROUND_CSZ_MIN 1u  // (A/B: the smallest sample chunk of a round's items)
-#endif
-#ifndef GS_ROUND_ITEMS_PER_LANE
-#define GS_ROUND_ITEMS_PER_LANE 8ull
-#endif
+        // (round 5: items of at least 2 or 4 samples, or 2 items per lane: +0.5%, -2.0%,
+        // -20% on A2, profiles/r05/ab_A2_round_item_sizes.txt)
         csz = min(16u, bs);
-        while (csz > GS_ROUND_CSZ_MIN && (uint64_t)n_seg * ((bs + csz - 1u) / csz) < GS_ROUND_ITEMS_PER_LANE * P->lanes)
-            csz >>= 1;
+        while (csz > 1u && (uint64_t)n_seg * ((bs + csz - 1u) / csz) < 8ull * P->lanes) csz >>= 1;
     }
     const uint32_t cpp = whole ? 1u : (bs + csz - 1u) / csz;
     P->per_sample = whole ? 0u : 1u;
