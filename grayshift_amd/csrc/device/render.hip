@@ -2679,9 +2679,12 @@ struct gs_device_scene {
     int32_t shade_batch = 52;                // finished lanes a wave shades together (scene's choice)
     int32_t cam_batch = 1;                   // lanes waiting for camera rays before a wave runs get_ray
     // A sample's cost on this device, lane-microseconds (kernel time x lanes / samples), from
-    // the frame context's last frame (gs_device_scene_note_frame); 0 = not measured yet.  The
-    // guided tail's small-frame rule reads it (launch).
+    // the frame context's last frame (gs_device_scene_note_frame); 0 = not measured yet.  Once
+    // a frame measured long samples, the guided tail's small-frame rule stays off for the
+    // scene (long_samples: sticky, so a scene near the threshold does not alternate layouts
+    // from frame to frame).
     std::atomic<double> lane_us_per_sample{0.0};
+    std::atomic<bool> long_samples{false};
     uint32_t node_records = 0, leaf_records = 0;
     double nodes_per_leaf = 0.0, other_leaf_frac = 0.0;
     // Launch state, mutated by launches of a const scene: guarded by `mu`.
@@ -3717,7 +3720,9 @@ static int device_cus(int dev) {
 void gs_device_scene_note_frame(gs_device_scene* ds, double kernel_ms, uint64_t samples) {
     if (!ds || !(kernel_ms > 0.0) || samples == 0) return;
     const double lanes = (double)device_cus(ds->device) * GS_BLOCK;
-    ds->lane_us_per_sample.store(kernel_ms * 1e3 * lanes / (double)samples, std::memory_order_relaxed);
+    const double lus = kernel_ms * 1e3 * lanes / (double)samples;
+    ds->lane_us_per_sample.store(lus, std::memory_order_relaxed);
+    if (lus > GS_SHORT_SAMPLE_LANE_US) ds->long_samples.store(true, std::memory_order_relaxed);
 }
 
 static bool part_ok(const gs_camera* cam, const gs_partition* p) {
@@ -3889,8 +3894,7 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
             // 14 047, cornell_box 8 272 / 8 918, perlin_spheres 1 524 / 3 320, simple_light
             // 1 056 / 2 762 (77-391 lane-us: their last 4-sample items drag the frame).
             const bool simple = (ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_MIXED)) == 0;
-            const double lus = ds->lane_us_per_sample.load(std::memory_order_relaxed);
-            const bool short_samples = lus == 0.0 || lus <= GS_SHORT_SAMPLE_LANE_US;
+            const bool short_samples = !ds->long_samples.load(std::memory_order_relaxed);
             const bool small = simple && short_samples && (uint64_t)cap * bs <= 4ull * lanes * c && t_pct == 0;
             const uint32_t fc_def = small ? std::min<uint32_t>(4u, c) : 1u;
             const uint32_t fc = std::max<uint32_t>(t_fc > 0 ? std::min<uint32_t>((uint32_t)t_fc, bs) : fc_def,
