@@ -25,7 +25,7 @@ pub const GS_REF_TRIANGLE: u32 = 5;
 pub const GS_REF_LIST: u32 = 6;
 pub const GS_REF_INSTANCE: u32 = 7;
 pub const GS_REF_MEDIUM: u32 = 8;
-pub const GS_ABI_VERSION: i32 = 10;
+pub const GS_ABI_VERSION: i32 = 11;
 pub const fn gs_make_ref(kind: u32, idx: u32) -> u32 { (kind << GS_REF_SHIFT) | (idx & 0x0FFF_FFFF) }
 
 #[repr(C)] #[derive(Clone, Copy, Default)]
@@ -138,7 +138,7 @@ pub struct gs_stats {
 pub struct gs_scene_info {
     pub node_records: u32, pub leaf_records: u32, pub lds_nodes: u32, pub lds_leaves: u32, pub lds_quads: u32,
     pub feat: i32, pub node_steps: i32, pub cert_boxes: i32, pub nodes_per_leaf: f64, pub other_leaf_frac: f64,
-    pub placement: i32, pub pad: i32, pub pilot_ms: f64,
+    pub placement: i32, pub long_samples: i32, pub pilot_ms: f64,
 }
 
 #[link(name = "grayshift")]
@@ -213,6 +213,7 @@ extern "C" {
     pub fn gs_multi_scene(m: *const gs_multi, rank: i32, scene: *mut *const gs_device_scene) -> gs_status;
     pub fn gs_multi_destroy(m: *mut gs_multi) -> gs_status;
     pub fn gs_debug_set_multi_collective(always: i32) -> gs_status;
+    pub fn gs_debug_set_multi_same_device(on: i32) -> gs_status;
 }
 
 pub fn last_error() -> String {

@@ -16,7 +16,7 @@ GS_OBJ_LIST, GS_OBJ_BVH, GS_OBJ_TRANSLATE, GS_OBJ_ROTATE_Y, GS_OBJ_CUBE, GS_OBJ_
 GS_MAT_LAMBERTIAN, GS_MAT_METAL, GS_MAT_DIELECTRIC, GS_MAT_DIFFUSE_LIGHT, GS_MAT_ISOTROPIC = 1, 2, 3, 4, 5
 GS_TEX_SOLID, GS_TEX_CHECKERED, GS_TEX_IMAGE, GS_TEX_NOISE = 1, 2, 3, 4
 GS_BG_SOLID, GS_BG_HDRI = 1, 2
-GS_ABI_VERSION = 10
+GS_ABI_VERSION = 11
 GS_OK, GS_ERR_ARG, GS_ERR_HIP, GS_ERR_OOM, GS_ERR_UNSUPPORTED, GS_ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5
 
 D3 = C.c_double * 3
@@ -149,7 +149,7 @@ class gs_scene_info(C.Structure):
     _fields_ = [("node_records", C.c_uint32), ("leaf_records", C.c_uint32), ("lds_nodes", C.c_uint32),
                 ("lds_leaves", C.c_uint32), ("lds_quads", C.c_uint32), ("feat", C.c_int32), ("node_steps", C.c_int32),
                 ("cert_boxes", C.c_int32), ("nodes_per_leaf", C.c_double), ("other_leaf_frac", C.c_double),
-                ("placement", C.c_int32), ("pad", C.c_int32), ("pilot_ms", C.c_double)]
+                ("placement", C.c_int32), ("long_samples", C.c_int32), ("pilot_ms", C.c_double)]
 
 
 # Every symbol include/*.h declares, with its ctypes signature.
@@ -209,6 +209,7 @@ SIGNATURES = {
     "gs_multi_scene": (C.c_int32, [_P, C.c_int32, C.POINTER(_P)]),
     "gs_multi_destroy": (C.c_int32, [_P]),
     "gs_debug_set_multi_collective": (C.c_int32, [C.c_int32]),
+    "gs_debug_set_multi_same_device": (C.c_int32, [C.c_int32]),
     # grayshift_host.h
     "gs_host_scene_from_spec": (C.c_int32, [C.POINTER(gs_scene_spec), C.POINTER(_P)]),
     "gs_host_scene_destroy": (C.c_int32, [_P]),

@@ -2353,15 +2353,33 @@ __global__ void gs_combine_kernel(const KParams* __restrict__ P) {
             continue;
         }
         const bool fine = k >= P->fine_px;
-        const uint32_t n = fine ? P->fine_cpp : cpp;
         // chunk-major sums: consecutive lanes read consecutive 24-B sums of each chunk
         const size_t stride = (size_t)(fine ? P->capacity - P->fine_px : P->fine_px) * 3;
         const double* p = P->partial + (fine ? (size_t)P->fine_base + (k - P->fine_px) : (size_t)k) * 3;
         double r = 0.0, g = 0.0, b = 0.0;
-        for (uint32_t c = 0; c < n; c++, p += stride) {
-            r += p[0];
-            g += p[1];
-            b += p[2];
+        if (!fine) {
+            for (uint32_t c = 0; c < cpp; c++, p += stride) {
+                r += p[0];
+                g += p[1];
+                b += p[2];
+            }
+        } else {
+            // 1-sample items (fine_chunk 1: each sum is 0 + s = s), re-formed into the coarse
+            // chunks of P->chunk samples and added in order: the coarse pixels' association,
+            // so a pixel's bits do not depend on whether its tile ran in the tail
+            const uint32_t bs = P->ss.batch_size, c = P->chunk;
+            for (uint32_t s0 = 0; s0 < bs; s0 += c) {
+                const uint32_t e = min(bs, s0 + c);
+                double cr = 0.0, cg = 0.0, cb = 0.0;
+                for (uint32_t s = s0; s < e; s++, p += stride) {
+                    cr += p[0];
+                    cg += p[1];
+                    cb += p[2];
+                }
+                r += cr;
+                g += cg;
+                b += cb;
+            }
         }
         const double cr = r / scount, cg = g / scount, cb = b / scount;
         if (o) {
@@ -2561,8 +2579,7 @@ static std::atomic<int32_t> g_node_steps{0};  // 0: the scene's own (gs_device_s
 // 4632, 12 -> 4648-4651, 14 -> 4624, 16 -> 4592; GS_KIND_LEAF_BATCH for kind-batched kernels)
 static std::atomic<int32_t> g_leaf_batch{0};
 static std::atomic<int32_t> g_cam_batch{0};  // 0: the scene's own (gs_set_camera_batch)
-static std::atomic<int32_t> g_fine_chunk{0};  // guided tail (gs_debug_set_guided_tail): 0 = default
-static std::atomic<int32_t> g_tail_pct{0};
+static std::atomic<int32_t> g_tail_pct{0};  // guided tail (gs_debug_set_guided_tail): 0 = default
 #ifndef GS_KIND_SHADE_BATCH
 #define GS_KIND_SHADE_BATCH 44
 #endif
@@ -3168,7 +3185,9 @@ gs_status gs_debug_set_partial_budget(uint64_t bytes) {
 
 gs_status gs_debug_set_guided_tail(int32_t fine_chunk, int32_t tail_pct) {
     if (fine_chunk < 0 || tail_pct < 0) return fail(GS_ERR_ARG, "fine_chunk and tail_pct are >= 0 (0: the default)");
-    g_fine_chunk.store(fine_chunk);
+    // (the tail's items are single samples, which the combine regroups into the coarse chunks:
+    // other sizes would make the association depend on which tiles run in the tail)
+    if (fine_chunk > 1) return fail(GS_ERR_ARG, "fine_chunk is 0 or 1 (1-sample tail items)");
     g_tail_pct.store(tail_pct);
     return GS_OK;
 }
@@ -3681,6 +3700,7 @@ gs_status gs_device_scene_info(const gs_device_scene* ds, gs_scene_info* out) {
     i.nodes_per_leaf = ds->nodes_per_leaf;
     i.other_leaf_frac = ds->other_leaf_frac;
     i.placement = ds->placement.load(std::memory_order_acquire);
+    i.long_samples = ds->long_samples.load(std::memory_order_relaxed) ? 1 : 0;
     i.pilot_ms = ds->pilot_ms;
     *out = i;
     return GS_OK;
@@ -3831,7 +3851,12 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     if (!part_ok(cam, part)) return fail(GS_ERR_ARG, "bad partition / image size");
     if (ss->batch_size == 0) return fail(GS_ERR_ARG, "batch_size 0 never terminates (camera.rs:137)");
     int64_t cap = gs_partition_capacity(cam, part);
-    if (cap <= 0) return GS_OK;
+    if (cap <= 0) {  // nothing to render; a frame context's counters still start from zero
+        if (zero_counters && d_counters) HIPCHK(hipMemsetAsync(d_counters, 0, sizeof(gs_counters), (hipStream_t)stream));
+        if (k_begin) HIPCHK(hipEventRecord(k_begin, (hipStream_t)stream));  // (a caller times an empty kernel span)
+        if (k_end) HIPCHK(hipEventRecord(k_end, (hipStream_t)stream));
+        return GS_OK;
+    }
     if (cap >= (int64_t)0xFFFFFFFFll) return fail(GS_ERR_ARG, "partition too large");
     if ((int64_t)cam->image_width * cam->image_height >= (int64_t)0xFFFFFFFFll)
         return fail(GS_ERR_ARG, "image too large for 32-bit pixel ids");
@@ -3853,62 +3878,68 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     kp.order = part->d_tile_order;
     // Split pixels into sample chunks only when the settings run exactly one batch:
     // max_samples < batch_size makes the first stop test (camera.rs:158) always true.
+    //
+    // What the frame's bits depend on (round 6): a pixel's
+    // colour is ((0 + C_0) + C_1) + ... over its chunks of c samples, each C_k = ((0 + s) + s)
+    // + ... in sample order, so the association is fixed by c alone -- and c is a function of
+    // the frame (W x H), the settings, the scene's flags and the process's knobs: never of the
+    // rank's capacity, the device count, the device's CUs or a timing.  How the samples are
+    // cut into work items is scheduling: the guided tail's 1-sample items (gs_combine_kernel
+    // re-forms their chunks of c: a 1-sample chunk sum is 0 + s = s, bit for bit, so the
+    // regrouped sum is the coarse chunk's) may sit on any tiles, sized by the rank's capacity,
+    // this device's lanes and the scene's measured cost, without changing a bit.
     const int32_t t_sample_chunk = g_sample_chunk.load(std::memory_order_relaxed);
     const uint64_t t_partial_budget = g_partial_budget.load(std::memory_order_relaxed);
     uint32_t chunk = 0, cpp = 1, fine_px = (uint32_t)cap, fine_chunk = 1, fine_cpp = 1;
     if (t_sample_chunk != 0 && ss->max_samples < ss->batch_size) {
         const uint32_t bs = ss->batch_size;
+        const uint64_t frame_px = (uint64_t)cam->image_width * (uint64_t)cam->image_height;
         uint32_t c = t_sample_chunk > 0 ? (uint32_t)t_sample_chunk : std::max<uint32_t>(16u, (bs + 63u) / 64u);
         if ((bs + c - 1) / c > 64u) c = (bs + 63u) / 64u;  // at most 64 chunks per pixel
-        if (t_sample_chunk < 0)
-            while (c < bs && (uint64_t)cap * ((bs + c - 1) / c) * 24u > t_partial_budget) c *= 2u;
-        const int32_t t_fc = g_fine_chunk.load(std::memory_order_relaxed);
+        if (t_sample_chunk < 0)  // (the whole frame's sums: the same c on every rank)
+            while (c < bs && frame_px * ((bs + c - 1) / c) * 24u > t_partial_budget) c *= 2u;
         const int32_t t_pct = g_tail_pct.load(std::memory_order_relaxed);
+        // A small frame -- at most twice the default tail's samples on a 256-CU device -- of a
+        // scene whose samples are alike (no media, no BVHs under instances, no staged shading)
+        // runs in chunks of 4 samples: there the items' fixed costs (claims, refills, chunk
+        // sums) outweigh the last chunk's length.  MI355X C1 (400x225 x 100 spp, earth + sky):
+        // 16-sample chunks with a 2-sample tail on 21 of 28 tiles 14 727, a 4-sample tail 16 579,
+        // every tile in 4-sample chunks 18 104 Msamples/s; 3, 5, 6 samples 15 977-17 205
+        // (profiles/r05/sweep_C1_guided_tail*.txt).  (A fixed lane count, not this device's:
+        // the chunk size is part of what the bits depend on.)
+        const bool simple = (ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_MIXED)) == 0;
+        const bool small = t_sample_chunk < 0 && t_pct == 0 && simple &&
+                           frame_px * bs <= 4ull * (256ull * GS_BLOCK) * std::min(c, bs);
+        if (small) c = std::min<uint32_t>(4u, c);
         if (t_sample_chunk < 0 || t_pct > 0) {  // (an explicit chunk with a tail: gs_debug_set_guided_tail)
             // Guided tail: a work item of c samples started just before the queue runs dry
             // can keep its lane busy for c samples while every other lane idles, and a frame
             // with few items per lane ends on them (MI355X final_scene 400x400 x 64 spp,
             // every pixel in chunks of 16: 211 Msamples/s; of 1: 1007).  So the rank's last
-            // tiles in queue order run in the finest chunks (at most 64 per pixel): enough
-            // tiles for 2 x lanes x c samples, which keeps the other lanes busy while the
-            // last coarse items finish.  Pixels with one chunk of all bs samples sum exactly
-            // like the unsplit loop, fine pixels of 1-sample chunks too.
-            c = std::min(c, bs);
-            const uint64_t tile_px = (uint64_t)part->tile_w * part->tile_h, slots = (uint64_t)cap / tile_px;
-            const uint64_t lanes = (uint64_t)std::max(1, device_cus(dev)) * GS_BLOCK;
-            // A small frame -- at most twice the default tail's samples -- of a scene whose
-            // samples are short and alike (no media, no BVHs under instances, no staged
-            // shading) runs wholly in fine chunks of 4 samples: there the items' fixed costs
-            // (claims, refills, chunk sums) outweigh the last chunk's length.  MI355X C1
-            // (400x225 x 100 spp, earth + sky): default tail of 2-sample chunks (21 of 28
-            // tiles) 14 727, 4-sample 16 579, every tile in 4-sample chunks 18 104 Msamples/s;
-            // 3, 5, 6 samples 15 977-17 205 (profiles/r05/sweep_C1_guided_tail*.txt).  Where
-            // samples vary (final_scene 400^2 x 64: every tile in 4-sample chunks 1 089, the
-            // 1-sample tail 1 381) and in larger frames (final_scene 1440^2 x 64: 1 sample
-            // 2 687, 4: 2 650) the tail keeps the finest chunks.
-            // Once a frame of the scene has been timed (the frame context), the rule also needs
-            // short samples: at most GS_SHORT_SAMPLE_LANE_US lane-microseconds each.  400-px
-            // reference scenes, rule on / off (profiles/r05/small_frame_rule_scenes.txt),
+            // tiles in queue order run in 1-sample items: enough tiles for 2 x lanes x c
+            // samples, which keeps the other lanes busy while the last coarse items finish.
+            // A small frame (above) takes no tail while its samples are short: once a frame of
+            // the scene measured more than GS_SHORT_SAMPLE_LANE_US lane-microseconds a sample
+            // (the frame context, gs_device_scene_note_frame; sticky) it takes the tail too.
+            // 400-px reference scenes, tail off / on (profiles/r05/small_frame_rule_scenes.txt),
             // Msamples/s: earth 17 317 / 8 725, hdri 13 956 / 7 100, triangles 14 582 / 8 465,
             // quads 13 402 / 11 088 (17-34 lane-us a sample) -- but checkered_spheres 10 523 /
             // 14 047, cornell_box 8 272 / 8 918, perlin_spheres 1 524 / 3 320, simple_light
-            // 1 056 / 2 762 (77-391 lane-us: their last 4-sample items drag the frame).
-            const bool simple = (ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_MIXED)) == 0;
+            // 1 056 / 2 762 (77-391 lane-us: their last 4-sample items drag the frame).  Being
+            // scheduling only, neither the timing nor the device's lanes change a bit.
+            c = std::min(c, bs);
+            const uint64_t tile_px = (uint64_t)part->tile_w * part->tile_h, slots = (uint64_t)cap / tile_px;
+            const uint64_t lanes = (uint64_t)std::max(1, device_cus(dev)) * GS_BLOCK;
             const bool short_samples = !ds->long_samples.load(std::memory_order_relaxed);
-            const bool small = simple && short_samples && (uint64_t)cap * bs <= 4ull * lanes * c && t_pct == 0;
-            const uint32_t fc_def = small ? std::min<uint32_t>(4u, c) : 1u;
-            const uint32_t fc = std::max<uint32_t>(t_fc > 0 ? std::min<uint32_t>((uint32_t)t_fc, bs) : fc_def,
-                                                   (bs + 63u) / 64u);  // (at most 64 chunks per pixel)
-            if (fc < c && slots > 0) {
-                const uint64_t want = small ? (uint64_t)cap * bs  // (every tile)
-                                            : lanes * c * (uint64_t)(t_pct > 0 ? t_pct : 200) / 100u;  // samples
+            if (c > 1 && slots > 0 && !(small && short_samples)) {
+                const uint64_t want = lanes * c * (uint64_t)(t_pct > 0 ? t_pct : 200) / 100u;  // samples
                 const uint64_t ft = std::min<uint64_t>(slots, (want + tile_px * bs - 1) / (tile_px * bs));
-                const uint32_t fpx = (uint32_t)((slots - ft) * tile_px), fcpp = (bs + fc - 1) / fc;
-                const uint64_t items = (uint64_t)fpx * ((bs + c - 1) / c) + ((uint64_t)cap - fpx) * fcpp;
+                const uint32_t fpx = (uint32_t)((slots - ft) * tile_px);
+                const uint64_t items = (uint64_t)fpx * ((bs + c - 1) / c) + ((uint64_t)cap - fpx) * bs;
                 if (items * 24u <= t_partial_budget && items < 0xFFFFFFFFull) {
                     fine_px = fpx;
-                    fine_chunk = fc;
-                    fine_cpp = fcpp;
+                    fine_chunk = 1;
+                    fine_cpp = bs;
                 }
             }
         }

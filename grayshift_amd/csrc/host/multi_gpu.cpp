@@ -154,6 +154,7 @@ struct DeviceGuard {
 };
 
 int g_collective_always = 0;  // gs_debug_set_multi_collective
+int g_same_device = 0;        // gs_debug_set_multi_same_device
 
 }  // namespace
 
@@ -161,6 +162,9 @@ struct gs_multi {
     std::vector<Device> dev;
     std::vector<int> ids;
     std::vector<ncclComm_t> comms;  // one rank per device (N > 1, or forced by the test hook)
+    // gs_debug_set_multi_same_device: N ranks on one device list that may repeat a device, the
+    // gather done by device copies on the ranks' streams instead of RCCL (N > 1, no comms)
+    bool copy_gather = false;
     bool comms_broken = false;      // a collective failed: the communicators were aborted
     int32_t tw = 64, th = 64;
     bool plan = false;
@@ -339,6 +343,27 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
         HIPOK(hipSetDevice(d0.id));
         src = gathered.p;
         src8 = gathered8.p;
+    } else if (copy_gather) {
+        // The test mode's gather (gs_debug_set_multi_same_device): each rank's packed tiles
+        // copied on its own stream into its rank-major slot of the first device's buffer,
+        // which ncclGather would fill the same way; the first device's stream waits for all.
+        if (want_rgb) GROW(gathered, (int64_t)n * cap * 12);
+        if (want8) GROW(gathered8, (int64_t)n * cap * 3);
+        for (int i = 0; i < n; i++) {
+            Device& d = dev[i];
+            HIPOK(hipSetDevice(d.id));
+            if (want_rgb)
+                HIPOK(hipMemcpyAsync((char*)gathered.p + (size_t)i * cap * 12, d.packed.p, (size_t)cap * 12,
+                                     hipMemcpyDeviceToDevice, d.stream));
+            if (want8)
+                HIPOK(hipMemcpyAsync((char*)gathered8.p + (size_t)i * cap * 3, d.packed8.p, (size_t)cap * 3,
+                                     hipMemcpyDeviceToDevice, d.stream));
+            HIPOK(hipEventRecord(d.ev[4], d.stream));
+        }
+        HIPOK(hipSetDevice(d0.id));
+        for (int i = 1; i < n; i++) HIPOK(hipStreamWaitEvent(d0.stream, dev[i].ev[4], 0));
+        src = gathered.p;
+        src8 = gathered8.p;
     }  // (no collective: the unpack is timed from the render's end event, ev[1])
     gs_partition pu{0, n, tw, th, order.empty() ? nullptr : (const int32_t*)d0.order.p, slots, 0};
     if (want_rgb && !direct) {
@@ -385,7 +410,7 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
     }
     HIPOK(hipSetDevice(d0.id));
     float gms = 0.0f;
-    if (timed_tail) HIPOK(hipEventElapsedTime(&gms, comms.empty() ? d0.ev[1] : d0.ev[4], d0.ev[5]));
+    if (timed_tail) HIPOK(hipEventElapsedTime(&gms, comms.empty() && !copy_gather ? d0.ev[1] : d0.ev[4], d0.ev[5]));
     have_rgb = want_rgb;
     have_rgb8 = want8;
     frame_w = cam->image_width;
@@ -412,7 +437,7 @@ gs_status gs_multi::render(const gs_camera* cam, const gs_sample_settings* ss, u
         stats->gather_ms = gms;
         stats->algorithmic_bytes = algorithmic_bytes(total);
         stats->gathered_bytes =
-            comms.empty() ? 0 : (uint64_t)n * (uint64_t)cap * ((want_rgb ? 12u : 0u) + (want8 ? 3u : 0u));
+            comms.empty() && !copy_gather ? 0 : (uint64_t)n * (uint64_t)cap * ((want_rgb ? 12u : 0u) + (want8 ? 3u : 0u));
         stats->num_gpus = n;
     }
     return GS_OK;
@@ -433,17 +458,18 @@ gs_status gs_multi_create(const gs_flat_scene* scene, const gs_launch* launch, g
     int visible = 0;
     if (hipGetDeviceCount(&visible) != hipSuccess || visible == 0) return fail(GS_ERR_NO_DEVICE, "no HIP device visible");
     const int n = launch->num_gpus > 0 ? launch->num_gpus : visible;
-    if (n > visible)
+    if (n > visible && !(g_same_device && launch->devices))  // (the test hook's lists may repeat a device)
         return fail(GS_ERR_ARG, "num_gpus " + std::to_string(n) + " > visible devices " + std::to_string(visible));
     std::vector<int> ids(n);
     for (int i = 0; i < n; i++) {
         ids[i] = launch->devices ? launch->devices[i] : i;
         if (ids[i] < 0 || ids[i] >= visible) return fail(GS_ERR_ARG, "bad device id");
-        for (int j = 0; j < i; j++)
+        for (int j = 0; j < i && !g_same_device; j++)
             if (ids[j] == ids[i]) return fail(GS_ERR_ARG, "device listed twice (one communicator rank per device)");
     }
     if (launch->tile_w < 0 || launch->tile_h < 0) return fail(GS_ERR_ARG, "negative tile size");
-    const bool collective = n > 1 || g_collective_always;
+    const bool copy_gather = g_same_device && n > 1;
+    const bool collective = !copy_gather && (n > 1 || g_collective_always);
     if (collective && !rccl().ok) return fail(GS_ERR_UNSUPPORTED, "RCCL unavailable: " + rccl().error);
     DeviceGuard guard;
     auto m = new gs_multi();
@@ -452,6 +478,7 @@ gs_status gs_multi_create(const gs_flat_scene* scene, const gs_launch* launch, g
     m->th = launch->tile_h > 0 ? launch->tile_h : m->tw;
     m->plan = launch->plan != 0;
     m->dev.resize(n);
+    m->copy_gather = copy_gather;
     auto bail = [&](gs_status st) {
         delete m;
         return st;
@@ -513,6 +540,12 @@ gs_status gs_multi_scene(const gs_multi* m, int32_t rank, const gs_device_scene*
 
 gs_status gs_debug_set_multi_collective(int32_t always) {
     g_collective_always = always ? 1 : 0;
+    return GS_OK;
+}
+
+gs_status gs_debug_set_multi_same_device(int32_t on) {
+    if (on != 0 && on != 1) return fail(GS_ERR_ARG, "same-device mode is 0 or 1");
+    g_same_device = on;
     return GS_OK;
 }
 

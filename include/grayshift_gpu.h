@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 10
+#define GS_ABI_VERSION 11
 
 typedef int32_t gs_status;
 enum {
@@ -294,12 +294,12 @@ gs_status gs_debug_set_cube_lists(int32_t on);
  * restores it).  A smaller budget makes renders take the chunk-doubling branch. */
 gs_status gs_debug_set_partial_budget(uint64_t bytes);
 
-/* Test hook (ABI 10): the auto sample-chunk rule's guided tail -- the samples per fine chunk
- * (0: the default, batch_size / 64 rounded up, at least 1) and how much of the frame runs in
- * fine chunks, as tail_pct percent of the device's lanes x the coarse chunk in samples (0:
- * the default, 200).  tail_pct > 0 also gives an explicit gs_set_tuning sample_chunk (the
- * coarse chunk) a tail.  Every choice renders the same samples; only the order in which a
- * pixel's chunk sums are added changes. */
+/* Test hook (ABI 10; ABI 11: fine_chunk 0 or 1 only): the auto sample-chunk rule's guided
+ * tail -- how much of the frame runs in 1-sample items, as tail_pct percent of the device's
+ * lanes x the coarse chunk in samples (0: the default, 200).  tail_pct > 0 also gives an
+ * explicit gs_set_tuning sample_chunk (the coarse chunk) a tail.  The tail is scheduling
+ * only: its items' sums are regrouped into the coarse chunks, so every choice renders the
+ * same bits.  fine_chunk > 1 is rejected (GS_ERR_ARG). */
 gs_status gs_debug_set_guided_tail(int32_t fine_chunk, int32_t tail_pct);
 
 /* Upload a flattened scene to the current HIP device. */
@@ -325,7 +325,9 @@ typedef struct gs_scene_info {
     double other_leaf_frac;
     int32_t placement;  /* (ABI 7) 0 static estimate, first launch pending; 1 static estimate (final);
                            2 measured by the first launch's pilot (gs_set_placement) */
-    int32_t pad;
+    int32_t long_samples; /* (ABI 11) 1 once a frame of the frame context measured more than 50 lane-us a
+                             sample (gs_multi_render's frame notes; sticky): small frames then take the
+                             guided tail's 1-sample items too -- scheduling only, the bits are unchanged */
     double pilot_ms;    /* (ABI 7) host time of that pilot and re-placement */
 } gs_scene_info;
 gs_status gs_device_scene_info(const gs_device_scene* scene, gs_scene_info* out);
@@ -490,6 +492,12 @@ gs_status gs_multi_destroy(gs_multi* m);
 /* Test hook: 1 = contexts created from now on use the RCCL communicator and gather even for
  * one device (so a one-GPU machine runs that code); 0 (default) = no collective for one. */
 gs_status gs_debug_set_multi_collective(int32_t always);
+/* Test hook (ABI 11): 1 = contexts created from now on accept a device list that repeats a
+ * device (launch->devices) and, for N > 1, gather the ranks' packed tiles by device copies on
+ * the ranks' streams instead of RCCL -- so a one-GPU machine runs the N-rank frame loop (one
+ * scene, stream and event set per rank, the plan, the concurrent launches, the rank-major
+ * unpack, the summed counters, per-rank frame notes) with N scenes on one device; 0 (default). */
+gs_status gs_debug_set_multi_same_device(int32_t on);
 
 /* Path of the RCCL library gs_render_multi uses (loaded on this call), or NULL. */
 const char* gs_rccl_library(void);

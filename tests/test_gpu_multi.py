@@ -276,7 +276,7 @@ def test_async_launch_returns_while_the_kernel_runs():
     frame before waiting for any, so a launch call must return while its kernel still runs,
     or the devices would serialise.  After a warm-up frame (the placement pilot and the
     slot's chunk-sum buffer are in place), the host call of a >= 100 ms C4 launch returns
-    in well under a millisecond, long before the stream drains."""
+    in a small fraction of the kernel's time, long before the stream drains."""
     import time
     torch = pytest.importorskip("torch")
     dev = torch.device("cuda", 0)
@@ -298,4 +298,5 @@ def test_async_launch_returns_while_the_kernel_runs():
     waits = [-c for c in calls if c < 0]
     r.close()
     assert min(waits) > 0.05, waits  # the frames did run long (>= ~100 ms of kernel)
-    assert max(launches) < 1e-3, launches
+    # (relative, not an absolute bound: a loaded host may take a few ms for the call itself)
+    assert max(launches) < 0.1 * min(waits), (launches, waits)

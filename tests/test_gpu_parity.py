@@ -323,13 +323,15 @@ def test_stated_spp_configs_vs_oracle(name, width, cpp):
 
 
 # ------------------------------------- the guided tail's knobs (gs_debug_set_guided_tail)
-@pytest.mark.parametrize("chunk,fine,pct", [(-1, 4, 1), (-1, 1, 10), (8, 2, 5), (-1, 0, 0), (-1, 2, 400)])
+@pytest.mark.parametrize("chunk,fine,pct", [(-1, 1, 1), (-1, 1, 10), (8, 1, 5), (-1, 0, 0), (-1, 1, 400)])
 def test_guided_tail_settings_vs_oracle(chunk, fine, pct):
     """C1's scene at 100 spp, 160x90 (six 64x64 tile slots) under other guided-tail settings:
     tails of 1 or 2 tiles (coarse and fine chunk sums both present: the chunk-major layout's
-    two regions, render.hip KParams.partial), fine chunks of 4, 1 or 2 samples, an explicit
-    8-sample coarse chunk with a tail, and the default and a 4x tail (every tile fine) --
-    against the oracle, counters exact."""
+    two regions, render.hip KParams.partial), an explicit 8-sample coarse chunk with a tail,
+    and the default and a 4x tail (every tile in 1-sample items) -- against the oracle,
+    counters exact.  The tail is scheduling only (round 6): its 1-sample sums are regrouped
+    into the coarse chunks, so the frame equals the same coarse chunking without a tail bit for
+    bit (auto chunks with a tail_pct: the 16-sample chunks; explicit 8: 8 without a tail)."""
     sc = scenes.config("C1", width=160)
     g.set_tuning(0, 0, 0, chunk)
     N.check(N.lib.gs_debug_set_guided_tail(fine, pct))
@@ -341,3 +343,11 @@ def test_guided_tail_settings_vs_oracle(chunk, fine, pct):
     ref, rc = oracle.render(sc, seed=23)
     assert gc["paths"] == sc.width * sc.height * sc.settings.batch_size
     assert maxdiff(out, ref) < TOL and counters_match(gc, rc)
+    if pct:
+        # the same coarse chunks with no tail at all (a 1-tile frame: a tail share of ~0)
+        g.set_tuning(0, 0, 0, 16 if chunk < 0 else chunk)
+        try:
+            plain, pc = g.render(sc, seed=23)
+        finally:
+            g.set_tuning(0, 0, 0, -1)
+        assert np.array_equal(out, plain) and pc == gc

@@ -39,7 +39,7 @@ def test_every_declared_symbol_is_exported(built):
 
 
 def test_version_and_error_channel():
-    assert N.lib.gs_version() == N.GS_ABI_VERSION == 10
+    assert N.lib.gs_version() == N.GS_ABI_VERSION == 11
     assert N.lib.gs_set_tuning(-1, 0, 0, -1) == N.GS_ERR_ARG
     assert b"tuning" in N.lib.gs_last_error()
     assert N.lib.gs_set_tuning(65, 0, 0, -1) == N.GS_ERR_ARG
@@ -47,12 +47,17 @@ def test_version_and_error_channel():
     assert N.lib.gs_set_tuning(60, 0, 8, -2) == N.GS_ERR_ARG
     assert N.lib.gs_set_tuning(60, 0, 8, -1) == N.GS_OK
     assert N.lib.gs_set_tuning(0, 0, 0, -1) == N.GS_OK  # (0: the scene's own shade batch, ABI 8)
-    # the guided tail's test hook (ABI 10): 0 = the defaults, negative values rejected
+    # the guided tail's test hook (ABI 10): 0 = the defaults, negative values rejected; ABI 11:
+    # tail items are single samples (other sizes would tie the bits to the tail's tiles)
     assert N.lib.gs_debug_set_guided_tail(-1, 0) == N.GS_ERR_ARG
     assert N.lib.gs_debug_set_guided_tail(0, -5) == N.GS_ERR_ARG
     assert b"fine_chunk" in N.lib.gs_last_error()
-    assert N.lib.gs_debug_set_guided_tail(4, 300) == N.GS_OK
+    assert N.lib.gs_debug_set_guided_tail(4, 300) == N.GS_ERR_ARG
+    assert N.lib.gs_debug_set_guided_tail(1, 300) == N.GS_OK
     assert N.lib.gs_debug_set_guided_tail(0, 0) == N.GS_OK
+    # the same-device frame-context hook (ABI 11)
+    assert N.lib.gs_debug_set_multi_same_device(2) == N.GS_ERR_ARG
+    assert N.lib.gs_debug_set_multi_same_device(0) == N.GS_OK
 
 
 @pytest.mark.parametrize("name", ["gs_object", "gs_material_spec", "gs_texture_spec", "gs_image_spec",
