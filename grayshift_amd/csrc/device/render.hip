@@ -79,6 +79,9 @@ using namespace gsd;
 #define GS_FEAT_VISITS 32 // count tests per threaded record (the placement pilot, run_pilot)
 #define GS_FEAT_SPHLEAF 64 // every top-level leaf is a stationary sphere (no media / nested BVHs):
                            // leaf passes without the other kinds' code or the kind test
+#define GS_FEAT_FIXED 128  // a fixed-spp launch in sample chunks (KParams.chunk != 0, no batch rounds,
+                           // max_depth > 0): the adaptive loop's batch ends, stop test, Σlum / Σlum²
+                           // and the rounds' per-sample colours are compiled out (round 6)
 #ifndef GS_NODE_STEPS
 #define GS_NODE_STEPS 8  // node steps per unrolled node pass (the render kernel, below)
 #endif
@@ -1243,7 +1246,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     extern __shared__ __align__(16) uint8_t smem[];
     // An empty batch round (adaptive settings: no active pixel left in this segment) has no
     // item to hand out: return before the mirror copy.
-    if (A.P->rounds && A.P->n_items == 0) return;
+    if (!(FEAT & GS_FEAT_FIXED) && A.P->rounds && A.P->n_items == 0) return;
 
     // The records a ray most likely tests (placed first by the host) are mirrored in LDS;
     // a lane whose node / leaf index is below lds_nodes / lds_leaves reads it from there
@@ -1290,6 +1293,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     // Every top-level leaf a stationary sphere: no instance is ever hit, so the hit's
     // instance (lane state L_HINST) stays GS_REF_NONE from the kernel's start.
     constexpr bool kSphLeaf = (FEAT & GS_FEAT_SPHLEAF) != 0;
+    // A fixed-spp chunked launch (the host's choice, kernel_for): P->chunk != 0, no rounds, no
+    // per-sample colours, max_depth > 0 -- a camera ray is always due when advance() runs.
+    constexpr bool kFixed = (FEAT & GS_FEAT_FIXED) != 0;
     // (t_in_lds kernels: the throughput's three fields first, at fixed offsets)
 #define LD(k) s_d[((k) + (t_in_lds(FEAT) ? 3 : 0)) * GS_BLOCK + tid]
 #define LI(k) s_i[(k) * GS_BLOCK + tid]
@@ -1347,7 +1353,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 
     // camera.rs:142-146 for one finished sample of colour L
     auto add_sample = [&](double Lr, double Lg, double Lb) {
-        if (P->per_sample) {  // batch rounds: the sample's colour, summed in order by the combine
+        if (!kFixed && P->per_sample) {  // batch rounds: the sample's colour, summed in order by the combine
             double* o = P->partial + (size_t)LI(L_ITEM) * 3;
             o[0] = Lr;
             o[1] = Lg;
@@ -1358,7 +1364,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             LD(L_CSG) += Lg;
             LD(L_CSB) += Lb;
         }
-        if (!P->chunk) {  // a chunk never reaches the stop test: Σlum, Σlum² unused
+        if (!kFixed && !P->chunk) {  // a chunk never reaches the stop test: Σlum, Σlum² unused
             double lum = 0.299 * Lr + 0.587 * Lg + 0.144 * Lb;
             LD(L_LSUM) += lum;
             LD(L_LSQ) += lum * lum;
@@ -1388,7 +1394,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     };
     auto end_chunk = [&]() {
         const uint32_t item = LI(L_ITEM);
-        if (!P->per_sample) {
+        if (kFixed || !P->per_sample) {
             double* o = P->partial + (size_t)item * 3;
             o[0] = LD(L_CSR);
             o[1] = LD(L_CSG);
@@ -1409,7 +1415,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     auto advance = [&]() {
 #pragma unroll 1
         for (;;) {
-            if (LI(L_BLEFT) == 0) {
+            // (fixed-spp launches: the shade pass ends a chunk at its last sample, so a lane
+            // here always has a sample left and max_depth > 0 -- straight to get_ray)
+            if (!kFixed && LI(L_BLEFT) == 0) {
                 if (P->chunk) {
                     end_chunk();
                     return;
@@ -1518,7 +1526,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #endif
             Tr = Tg = Tb = 1.0;
             LI(L_DEPTH) = cam.max_depth;
-            if (cam.max_depth > 0) {
+            if (kFixed || cam.max_depth > 0) {
                 fresh = true;  // begin_ray by the caller
                 st = S_TRACE;
                 return;
@@ -1622,7 +1630,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     const uint32_t qr = fine ? q32 - P->fine_base : q32;
                     const uint32_t pr = udiv(qr, fine ? P->u_fcpp : P->u_cpp), ck = qr - pr * cpp;
                     uint32_t slot, x, y;
-                    if (P->rounds) {  // batch rounds: the packed pixel of active entry pr
+                    if (!kFixed && P->rounds) {  // batch rounds: the packed pixel of active entry pr
                         const uint32_t it = P->active[P->seg_base + pr];
                         slot = udiv(it, P->u_tpx);
                         const uint32_t w = it - slot * tile_px;
@@ -1649,7 +1657,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     const uint32_t pi = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu : tx * (uint32_t)P->tile_w + x;
                     const uint32_t pj = tile == 0xFFFFFFFFu ? 0xFFFFFFFFu : ty * (uint32_t)P->tile_h + y;
                     if (pi >= (uint32_t)cam.image_width || pj >= (uint32_t)cam.image_height) {
-                        if (!P->chunk && !P->direct) {  // padding pixel (chunked: gs_combine_kernel writes it)
+                        if (!kFixed && !P->chunk && !P->direct) {  // padding pixel (chunked: gs_combine_kernel writes it)
                             if (P->out) {
                                 float* o = P->out + (size_t)item * 3;
                                 o[0] = 0.0f;
@@ -1668,12 +1676,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         LD(L_CSR) = 0.0;
                         LD(L_CSG) = 0.0;
                         LD(L_CSB) = 0.0;
-                        if (P->per_sample) {
+                        if (!kFixed && P->per_sample) {
                             // batch rounds: the sample slots of entry pr, samples ck * csz on
                             LI(L_ITEM) = ck * csz * P->seg_n + pr;
                             LI(L_SAMPLE) = P->round_base + ck * csz;
                             LI(L_BLEFT) = min(csz, P->ss.batch_size - ck * csz);
-                        } else if (P->chunk) {
+                        } else if (kFixed || P->chunk) {
                             // chunk sums, chunk-major: a coarse pixel's at ck * fine_px + item,
                             // a fine one's after every coarse pixel's (the packed pixel and its
                             // queue position share a tile, so both are in the fine region or neither)
@@ -2240,7 +2248,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             if (ends) {  // the sample is done; its item's next camera ray comes at the loop head
                 GS_STAMP(r0);
                 add_sample(Lr, Lg, Lb);
-                if (P->chunk && LI(L_BLEFT) == 0) end_chunk();  // -> S_NEED
+                if ((kFixed || P->chunk) && LI(L_BLEFT) == 0) end_chunk();  // -> S_NEED
                 else st = S_CAM;
                 GS_REGION(4, r0);
             }
@@ -3766,32 +3774,33 @@ static void (*kernel_for(int feat))(KArgs) {
     (void)feat;
     return gs_render_kernel<GS_ONLY_FEAT>;
 #else
+    // The product instantiations, each also in its fixed-spp form (| GS_FEAT_FIXED).
+#define GS_K(F)                                              \
+    case (F): return gs_render_kernel<(F)>;                  \
+    case (F) | GS_FEAT_FIXED: return gs_render_kernel<(F) | GS_FEAT_FIXED>;
     switch (feat) {
-        case GS_FEAT_MEDIA: return gs_render_kernel<GS_FEAT_MEDIA>;
-        case GS_FEAT_NESTED: return gs_render_kernel<GS_FEAT_NESTED>;
-        case GS_FEAT_MEDIA | GS_FEAT_NESTED: return gs_render_kernel<GS_FEAT_MEDIA | GS_FEAT_NESTED>;
-        case GS_FEAT_LEAFRUN: return gs_render_kernel<GS_FEAT_LEAFRUN>;
-        case GS_FEAT_LEAFRUN | GS_FEAT_MEDIA: return gs_render_kernel<GS_FEAT_LEAFRUN | GS_FEAT_MEDIA>;
-        case GS_FEAT_LEAFRUN | GS_FEAT_NESTED: return gs_render_kernel<GS_FEAT_LEAFRUN | GS_FEAT_NESTED>;
-        case GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED:
-            return gs_render_kernel<GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED>;
-        case GS_FEAT_LDSTREE: return gs_render_kernel<GS_FEAT_LDSTREE>;
-        case GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN: return gs_render_kernel<GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN>;
-        case GS_FEAT_MIXED: return gs_render_kernel<GS_FEAT_MIXED>;
-        case GS_FEAT_MIXED | GS_FEAT_LEAFRUN: return gs_render_kernel<GS_FEAT_MIXED | GS_FEAT_LEAFRUN>;
-        case GS_FEAT_MIXED | GS_FEAT_LDSTREE: return gs_render_kernel<GS_FEAT_MIXED | GS_FEAT_LDSTREE>;
-        case GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN:
-            return gs_render_kernel<GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN>;
+        GS_K(GS_FEAT_MEDIA)
+        GS_K(GS_FEAT_NESTED)
+        GS_K(GS_FEAT_MEDIA | GS_FEAT_NESTED)
+        GS_K(GS_FEAT_LEAFRUN)
+        GS_K(GS_FEAT_LEAFRUN | GS_FEAT_MEDIA)
+        GS_K(GS_FEAT_LEAFRUN | GS_FEAT_NESTED)
+        GS_K(GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED)
+        GS_K(GS_FEAT_LDSTREE)
+        GS_K(GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN)
+        GS_K(GS_FEAT_MIXED)
+        GS_K(GS_FEAT_MIXED | GS_FEAT_LEAFRUN)
+        GS_K(GS_FEAT_MIXED | GS_FEAT_LDSTREE)
+        GS_K(GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN)
+        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN)
+        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_LDSTREE)
+        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED)
+        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_LDSTREE)
+        case GS_FEAT_FIXED: return gs_render_kernel<GS_FEAT_FIXED>;
         case GS_FEAT_PILOT: return gs_render_kernel<GS_FEAT_PILOT>;
-        case GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN: return gs_render_kernel<GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN>;
-        case GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_LDSTREE:
-            return gs_render_kernel<GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_LDSTREE>;
-        case GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED:
-            return gs_render_kernel<GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED>;
-        case GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_LDSTREE:
-            return gs_render_kernel<GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_LDSTREE>;
         default: return gs_render_kernel<0>;
     }
+#undef GS_K
 #endif
 }
 
@@ -4075,7 +4084,11 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     const uint64_t waves = (uint64_t)blocks * (GS_BLOCK / 64);
     kp.waves = (uint32_t)waves;
     kp.lanes = (uint32_t)(blocks * GS_BLOCK);
-    kp.claim = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, (uint64_t)kp.n_items / waves / GS_CLAIM_DIV));
+    // (coarse items of at most 4 samples -- a small frame's chunks -- claim like the tail's: the
+    // one queue counter serialises claims of 32; MI355X C1, 4-sample items: 32 -> 1.15 ms, 128 ->
+    // 0.57 ms a frame)
+    const uint64_t claim_cap = kp.chunk && kp.chunk <= 4u ? (uint64_t)GS_CLAIM_FINE : 32u;
+    kp.claim = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(claim_cap, (uint64_t)kp.n_items / waves / GS_CLAIM_DIV));
     kp.claim_fine = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(GS_CLAIM_FINE, (uint64_t)kp.n_items / waves / GS_CLAIM_DIV));
     // The u32 queue counter runs past n_items by at most one claim per wave (each wave's
     // last, failed claim): it must not wrap.
@@ -4186,7 +4199,13 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     }
     if (k_begin) HIPCHK(hipEventRecord(k_begin, st));
     const bool pilot_kernel = va != nullptr;
-    hipLaunchKernelGGL(kernel_for(pilot_kernel ? GS_FEAT_PILOT : lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
+    // (a fixed-spp chunked launch takes the instantiation without the adaptive paths)
+#ifndef GS_USE_FIXED
+#define GS_USE_FIXED 1  // (A/B: 0 launches the generic instantiation for fixed-spp frames too)
+#endif
+    const bool fixed = GS_USE_FIXED && kp.chunk != 0 && !n_rounds && cam->max_depth > 0;
+    hipLaunchKernelGGL(kernel_for(pilot_kernel ? GS_FEAT_PILOT : lc.feat | (fixed ? GS_FEAT_FIXED : 0)), dim3((unsigned)blocks),
+                       dim3(GS_BLOCK), lds, st, a);
     HIPCHK(hipGetLastError());
     if (k_end) HIPCHK(hipEventRecord(k_end, st));
     if (chunk) {
