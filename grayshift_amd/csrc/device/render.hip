@@ -79,6 +79,9 @@ using namespace gsd;
 #define GS_FEAT_VISITS 32 // count tests per threaded record (the placement pilot, run_pilot)
 #define GS_FEAT_SPHLEAF 64 // every top-level leaf is a stationary sphere (no media / nested BVHs):
                            // leaf passes without the other kinds' code or the kind test
+#define GS_FEAT_PLAIN 256  // staged shading of sphere-only trees whose materials are all solid / two-solid
+                           // checker Lambertians, metals and dielectrics with no uv: the hit record of a
+                           // stationary sphere only, no texture, light or isotropic code (round 6; C4)
 #define GS_FEAT_FIXED 128  // a fixed-spp launch in sample chunks (KParams.chunk != 0, no batch rounds,
                            // max_depth > 0): the adaptive loop's batch ends, stop test, Σlum / Σlum²
                            // and the rounds' per-sample colours are compiled out (round 6)
@@ -817,6 +820,24 @@ __device__ GS_NOINLINE HitRec reconstruct(const DevScene& sc, Ray r, double t, u
     return h;
 }
 
+// The same for a hit that can only be a stationary sphere with a material that needs no uv
+// (GS_FEAT_PLAIN): reconstruct's sphere branch and HitRecord::new, nothing else.
+__device__ __forceinline__ HitRec reconstruct_sphere(const DevScene& sc, const Ray& r, double t, uint32_t hit_ref) {
+    HitRec h;
+    const uint32_t idx = hit_ref & GS_REF_MASK;
+    const DSphere s = sc.spheres[idx];
+    const d3 c = mk(s.cx, s.cy, s.cz);
+    h.mat = sc.sphere_mat[idx];
+    const d3 p = add(r.o, muls(r.d, t));
+    const d3 outward = divs(sub(p, c), s.r);
+    h.front = dot(r.d, outward) < 0.0;  // hittable.rs:26-43
+    h.n = h.front ? outward : neg(outward);
+    h.p = p;
+    h.u = 0.0;
+    h.v = 0.0;
+    return h;
+}
+
 // Texture::value_at (texture.rs:27-95); checkered nesting resolved iteratively.
 __device__ GS_NOINLINE d3 texture_value(const DevScene& sc, uint32_t tex, double u, double v, d3 p,
                                          unsigned long long* cnt) {
@@ -905,6 +926,7 @@ struct ShadeOut {
 // in the same order; only which lanes issue an instruction together changes.
 // A hit lane's ray.o becomes the hit point p (the next ray's origin) as soon as p is
 // known: nothing after the HitRecord reads the old origin, and p need not stay live.
+template <bool PLAIN>
 __device__ __forceinline__ ShadeOut shade(const DevScene& sc, Ray& ray, double t, uint32_t hit_ref,
                                           uint32_t hit_inst, uint64_t& rng, unsigned long long* cnt) {
     const double PI = 3.14159265358979323846;
@@ -921,7 +943,7 @@ __device__ __forceinline__ ShadeOut shade(const DevScene& sc, Ray& ray, double t
     const DMaterial* m = sc.mats;
     if (!miss) {
         atomicAdd(&cnt[C_HITS], 1ull);
-        h = reconstruct(sc, ray, t, hit_ref, hit_inst);
+        h = PLAIN ? reconstruct_sphere(sc, ray, t, hit_ref) : reconstruct(sc, ray, t, hit_ref, hit_inst);
         m = &sc.mats[h.mat];
         kind = m->kind;
         ray.o = h.p;
@@ -929,11 +951,11 @@ __device__ __forceinline__ ShadeOut shade(const DevScene& sc, Ray& ray, double t
     const bool lamb = kind >= DM_LAMB_SOLID && kind <= DM_LAMB_TEX;  // material.rs:45-68
     const bool metal = kind == DM_METAL;                              // :87-102
     const bool diel = kind == DM_DIELECTRIC;                          // :123-148
-    const bool iso = kind == DM_ISO_SOLID || kind == DM_ISO_TEX;      // :185-196
+    const bool iso = !PLAIN && (kind == DM_ISO_SOLID || kind == DM_ISO_TEX);  // :185-196
     const bool sky = miss && sc.bg.kind != GS_BG_SOLID;
 
     // albedo / emitted colour (texture.rs:27-95): one texture_value call site for every kind
-    if (kind == DM_LAMB_TEX || kind == DM_LIGHT_TEX || kind == DM_ISO_TEX) {
+    if (!PLAIN && (kind == DM_LAMB_TEX || kind == DM_LIGHT_TEX || kind == DM_ISO_TEX)) {
         o.col = texture_value(sc, m->texture, h.u, h.v, h.p, cnt);
     } else if (kind == DM_LAMB_CHECKER) {
         o.col = checker(*m, h.p);
@@ -2180,12 +2202,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     uint64_t g2 = rng;
                     double c2 = closest;
                     asm volatile("" : "+v"(r2.d.x), "+v"(c2));
-                    const ShadeOut s2 = shade(sc, r2, c2, hit_ref, LI(L_HINST), g2, s_cnt);
+                    const ShadeOut s2 = shade<(FEAT & GS_FEAT_PLAIN) != 0>(sc, r2, c2, hit_ref, LI(L_HINST), g2, s_cnt);
                     asm volatile("" ::"v"(s2.col.x), "v"(s2.col.y), "v"(s2.col.z), "v"(s2.dir.x), "v"(s2.dir.y), "v"(s2.dir.z),
                                  "v"(r2.o.x), "v"(g2), "v"(s2.cont));
                 }
 #endif
-                const ShadeOut s = shade(sc, ray, closest, hit_ref, LI(L_HINST), rng, s_cnt);
+                const ShadeOut s = shade<(FEAT & GS_FEAT_PLAIN) != 0>(sc, ray, closest, hit_ref,
+                                                                      (FEAT & GS_FEAT_PLAIN) ? GS_REF_NONE : LI(L_HINST), rng, s_cnt);
                 GS_MARK("shade_end");
                 GS_REGION(2, r0);
                 if (s.cont) {
@@ -2809,6 +2832,10 @@ static bool aligned_tquad(const gs_quad& q, TQuad& out) {
 }
 
 static std::atomic<int32_t> g_cube_lists{1};  // gs_debug_set_cube_lists
+#ifndef GS_PLAIN_KERNELS
+#define GS_PLAIN_KERNELS 1  // (A/B: 0 keeps C4 on the generic staged shading)
+#endif
+static const bool g_plain_kernels = GS_PLAIN_KERNELS;
 // A Quad::cube list's device record (cube_test): six consecutive quads whose aligned forms
 // carry cube_code(k) in order and equal, field by field, what cube_src derives from the 12
 // numbers taken from them.  Returns false (the list keeps the loop) otherwise.
@@ -3667,6 +3694,14 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         if (cases >= 3 && !(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED))) ds->feat |= GS_FEAT_MIXED;
     }
     if (sph_leaves && leaf_runs && !(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED))) ds->feat |= GS_FEAT_SPHLEAF;
+    if ((ds->feat & (GS_FEAT_SPHLEAF | GS_FEAT_MIXED)) == (GS_FEAT_SPHLEAF | GS_FEAT_MIXED) && g_plain_kernels) {
+        // every hit a stationary sphere (SPHLEAF): plain materials, no uv -> GS_FEAT_PLAIN
+        bool plain = true;
+        for (const DMaterial& m : mats)
+            plain &= (m.kind == DM_LAMB_SOLID || m.kind == DM_LAMB_CHECKER || m.kind == DM_METAL ||
+                      m.kind == DM_DIELECTRIC) && !m.needs_uv;
+        if (plain) ds->feat |= GS_FEAT_PLAIN;
+    }
     ds->cert_boxes = cert_boxes;
     ds->node_steps = auto_node_steps;
     // Scenes with BVHs under instances (kind-batched leaf passes over many leaf kinds) gather
@@ -3796,6 +3831,8 @@ static void (*kernel_for(int feat))(KArgs) {
         GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_LDSTREE)
         GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED)
         GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_LDSTREE)
+        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_PLAIN)
+        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_PLAIN | GS_FEAT_LDSTREE)
         case GS_FEAT_FIXED: return gs_render_kernel<GS_FEAT_FIXED>;
         case GS_FEAT_PILOT: return gs_render_kernel<GS_FEAT_PILOT>;
         default: return gs_render_kernel<0>;
