@@ -153,7 +153,10 @@ __device__ __forceinline__ bool box_hit_fast(const DNode& n, const d3& o, const 
 // f64 product, rounded once), R = max over axes |o * (1/d)|.  Per plane: t' = fma(m32,
 // ix, ox) with m32 = f32(m).  For the exact t = (m - o) / d and u = 2^-24:
 //   |t' - t| <= u|t| (fma) + (2u + u^2)|m (1/d)| + u R  <=  3.01u (|t| + R)
-// since |m (1/d)| <= |t| + R.  The f64 value the reference computes is within 2^-52 |t|
+// since |m (1/d)| <= |t| + R.  (Round 6: 1/d is the hardware reciprocal refined by two Newton
+// steps, rcp_cert below, within 2^-50 |1/d| of the exact value for a normal d: that
+// adds at most 2^-49 |m (1/d)| + 2^-50 R, under 2^-30 (|t| + R), to the terms above, and the
+// 3.01u bound, like K below, has room for 0.01u = 2^-30.6.)  The f64 value the reference computes is within 2^-52 |t|
 // of t.  lo = max(tmin, per-axis minima), hi = min(closest, per-axis maxima): x - k(|x|
 // + R) and x + k(|x| + R) are increasing in x for k < 1, so a max / min of values each
 // within k(|v'| + R) of its target is within k(|result'| + R) of the target's max / min;
@@ -204,6 +207,18 @@ struct RayCert {
     float r2;        // 2 K R + 1e-30
 };
 
+// 1/d for the certified test's constants only (make_cert, cert_ray_ok; round 6): the hardware
+// reciprocal and two Newton steps, within ~2^-52 of 1/d for a normal, finite d -- the
+// certificate's bound needs 2^-31 (above) -- in 5 instructions instead of a correctly
+// rounded division's 11.  A zero, infinite or denormal component gives a NaN or infinity,
+// which cert_ray_ok rejects (the ray then takes the f64 test, whose 1/d is render.hip's inv_of, an exact division).
+__device__ __forceinline__ double rcp_cert(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-d, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
 __host__ __device__ __forceinline__ bool cert_ray_ok(const d3& o, const d3& inv) {
     auto ok_inv = [](double v) { return __builtin_fabs(v) <= 1e15 && __builtin_fabs(v) >= 1e-25; };
     auto ok_o = [](double v) { return __builtin_fabs(v) <= 1e15; };

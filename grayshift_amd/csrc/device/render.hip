@@ -347,6 +347,10 @@ __device__ __forceinline__ d3 inv_of(d3 d) {
     asm volatile("" : "+v"(d.x), "+v"(d.y), "+v"(d.z));
     return mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
 }
+__device__ __forceinline__ d3 inv_cert(d3 d) {
+    asm volatile("" : "+v"(d.x), "+v"(d.y), "+v"(d.z));  // (as inv_of: not hoisted)
+    return mk(rcp_cert(d.x), rcp_cert(d.y), rcp_cert(d.z));
+}
 // A leaf record: the sphere's centre and radius squared, its next link and its ABI ref.
 template <bool LDS_ONLY>
 __device__ __forceinline__ void load_tleaf(const uint8_t* s_leaves, const TLeaf* g, uint32_t i, uint32_t lds_l,
@@ -1361,8 +1365,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     uint32_t c_nodes = 0, c_sph = 0;  // (per lane: one VALU add beat a 64-bit SALU wave count)
 
     auto begin_ray = [&]() {
-        // AABB::hit's `1.0 / ray.direction[axis]` (AABB.rs:64), hoisted per ray (same value)
-        const d3 inv = mk(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
+        // AABB::hit's `1.0 / ray.direction[axis]` (AABB.rs:64), hoisted per ray for the certified
+        // f32 test's constants (rcp_cert: within 2^-52 of it; the f64 test takes inv_of's exact one)
+        const d3 inv = inv_cert(ray.d);
         fast = A.cert_boxes && cert_ray_ok(ray.o, inv);
         rc = make_cert(ray.o, inv);
         cur = A.root;  // the root record's link (THR_*)
@@ -1938,6 +1943,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 // chain ended (the tree's last links are THR_RET) takes back its top-level ray
                 // and goes on at the record after the instance's leaf -- where BVHNode::hit's
                 // recursion returns from the Translate / RotateY's hit (hittable.rs:107-211).
+#ifdef GS_STAMPS
+                uint64_t rt0_;
+                GS_STAMP(rt0_);
+#endif
                 if (cur == THR_RET) {
                     const double* sv = P->nest_save + ((size_t)blockIdx.x * GS_BLOCK + tid) * 8u;
                     ray.o = mk(sv[0], sv[1], sv[2]);
@@ -1945,6 +1954,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     cur = (uint32_t)__double_as_longlong(sv[6]);
                     LNINST = GS_REF_NONE;
                 }
+                GS_REGION(6, rt0_);  // (stamps: return passes)
             } else if (at_leaf) {
                 GS_MARK("leaf_begin");
                 double scx, scy, scz, sr;
@@ -2160,12 +2170,17 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             if constexpr ((FEAT & GS_FEAT_NESTED) != 0 ||
                           (FEAT & (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)) == (GS_FEAT_MEDIA | GS_FEAT_LEAFRUN)) {
                 if (leaf_pass) {
-                    const d3 inv = inv_of(ray.d);
+#ifdef GS_STAMPS
+                    uint64_t rc0_;
+                    GS_STAMP(rc0_);
+#endif
+                    const d3 inv = inv_cert(ray.d);
                     rc = make_cert(ray.o, inv);
                     if constexpr (kNested) {
                         fast = A.cert_boxes && cert_ray_ok(ray.o, inv);
                         wave_fast = __builtin_amdgcn_ballot_w64(cur != THR_END && !fast) == 0;
                     }
+                    GS_REGION(5, rc0_);  // (stamps: the recomputation's share of the leaf-pass clock)
                 }
             }
 #ifdef GS_STAMPS
@@ -2305,6 +2320,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         atomicAdd(&dbg[9], (unsigned long long)ln_shade);
         for (int k = 0; k < 5; k++) atomicAdd(&dbg[10 + k], s_reg[(tid >> 6) * 16 + k]);
         for (int k = 0; k < 8; k++) atomicAdd(&dbg[24 + k], s_reg[(tid >> 6) * 16 + 8 + k]);
+        for (int k = 5; k < 7; k++) atomicAdd(&dbg[29 + k], s_reg[(tid >> 6) * 16 + k]);  // dbg[34], dbg[35]
         atomicAdd(&dbg[15], (unsigned long long)acc_node);
         atomicAdd(&dbg[16], (unsigned long long)acc_leaf);
         atomicAdd(&dbg[20], (unsigned long long)d_wsteps);

@@ -37,18 +37,29 @@ __global__ void k_aabb_cert(int n, const double* box, const double* ray, const d
     d3 inv = mk(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
     bool boxes_ok = true;
     for (int k = 0; k < 6; k++) boxes_ok = boxes_ok && __builtin_fabs(b[k]) <= 1e15;
-    if (!boxes_ok || !cert_ray_ok(o, inv)) {
+    // (the product's constants: the refined hardware reciprocal, rcp_cert; the f64 test below
+    // keeps the exact 1/d, as the megakernel's inv_of)
+    const d3 invc = mk(rcp_cert(d.x), rcp_cert(d.y), rcp_cert(d.z));
+    if (!boxes_ok || !cert_ray_ok(o, invc)) {
         out[i] = -1;
         dec[i] = -1;
         return;
     }
-    const RayCert rc = make_cert(o, inv);
+    const RayCert rc = make_cert(o, invc);
     bool und;
     bool h = box_cert((float)b[0], (float)b[1], (float)b[2], (float)b[3], (float)b[4], (float)b[5], rc,
                       (float)iv[2 * i], (float)iv[2 * i + 1], und);
     dec[i] = und ? 2 : (h ? 1 : 0);
     if (und) h = box_hit_fast(nd, o, inv, iv[2 * i], iv[2 * i + 1]);
     out[i] = h ? 1 : 0;
+}
+
+// rcp_cert (the certified test's 1/d) next to the exact division, per case.
+__global__ void k_rcp_cert(int n, const double* d, double* approx, double* exact) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    approx[i] = rcp_cert(d[i]);
+    exact[i] = 1.0 / d[i];
 }
 
 __global__ void k_sphere(int n, const double* sph, const double* ray, const double* iv, double* t, int* hit) {
@@ -170,6 +181,16 @@ int kat_aabb_cert(int n, const double* box, const double* ray, const double* iv,
     back(out, dout, n);
     back(dec, ddec, n);
     (void)hipFree(db); (void)hipFree(dr); (void)hipFree(di);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+int kat_rcp_cert(int n, const double* d, double* approx, double* exact) {
+    double* dd = dcopy(d, n);
+    double *da = dcopy<double>(nullptr, n), *de = dcopy<double>(nullptr, n);
+    hipLaunchKernelGGL(k_rcp_cert, grid(n), dim3(256), 0, 0, n, dd, da, de);
+    back(approx, da, n);
+    back(exact, de, n);
+    (void)hipFree(dd);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 

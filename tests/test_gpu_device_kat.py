@@ -23,7 +23,8 @@ def kat(built):
                     "kat_tri": [C.c_int, P, P, P, P], "kat_rng": [C.c_int, P, P, P, C.c_int, P],
                     "kat_math": [C.c_int, C.c_int, P, P, P],
                     "kat_noise": [C.c_int, C.c_int, P, C.c_double, P, P],
-                    "kat_sky": [C.c_int, C.c_uint32, C.c_uint32, P, P]}.items():
+                    "kat_sky": [C.c_int, C.c_uint32, C.c_uint32, P, P],
+                    "kat_rcp_cert": [C.c_int, P, P, P]}.items():
         getattr(L, f).argtypes = args
         getattr(L, f).restype = C.c_int
     return L
@@ -247,3 +248,28 @@ def test_noise_texture_value_within_libm_ulps(kat):
         assert kat.kat_noise(n, 1, ptr(perm), scale, ptr(p), ptr(out)) == 0
         ref = np.array([oracle.noise_value(scale, q) for q in p])
         assert np.abs(out - ref).max() <= 4 * np.spacing(1.0)
+
+
+def test_rcp_cert_within_the_certificates_bound(kat):
+    """rcp_cert (geometry.hpp, round 6): the certified test's 1/d from the hardware reciprocal
+    and two Newton steps must be within 2^-50 of the exact quotient over the cert range (|1/d|
+    in [1e-25, 1e15]); outside it -- zeros, infinities, denormals -- it must give a value
+    cert_ray_ok rejects (NaN, an infinity, or a magnitude out of range), never a finite
+    in-range wrong one."""
+    rng = np.random.default_rng(7)
+    n = 400000
+    mant = rng.uniform(1.0, 2.0, n) * np.where(rng.random(n) < 0.5, -1.0, 1.0)
+    d = mant * np.exp2(rng.integers(-83, 50, n)).astype(np.float64)
+    d[:8] = [0.0, -0.0, np.inf, -np.inf, 5e-324, -1e-310, 1e-16, 1e26]
+    d = np.ascontiguousarray(d)
+    approx, exact = np.zeros(n), np.zeros(n)
+    assert kat.kat_rcp_cert(n, ptr(d), ptr(approx), ptr(exact)) == 0
+    with np.errstate(all="ignore"):
+        inrange = (np.abs(exact) <= 1e15) & (np.abs(exact) >= 1e-25)
+        rel = np.abs(approx[inrange] - exact[inrange]) / np.abs(exact[inrange])
+        assert rel.max() <= 2.0 ** -50, rel.max()
+        ok = lambda v: (np.abs(v) <= 1e15) & (np.abs(v) >= 1e-25)
+        # a component clearly outside the range (zero, infinite, denormal, or 2x past a bound) is
+        # rejected with the approximate value too; at a bound either choice is sound (the f64 test)
+        out = ~((np.abs(exact) <= 2e15) & (np.abs(exact) >= 0.5e-25))
+        assert out[:8].sum() >= 6 and not ok(approx[out]).any()

@@ -63,6 +63,10 @@ def main():
         names = ["node", "sphere", "msphere", "quad", "triangle", "list", "instance", "medium"]
         print("leaf-kind clock (%% of leaf-pass clock; a pass's non-sphere branch by its first lane's ref kind): " +
               "  ".join("%s %.1f%%" % (n, 100.0 * x / max(1, leaf_clk)) for n, x in zip(names, kinds) if x))
+    rc_clk, ret_clk = dbg[34:36].cpu().tolist()
+    if rc_clk or ret_clk:
+        print("leaf passes of nested / media-run kernels: cert constants recomputed %.1f%%, return passes %.1f%% "
+              "of the leaf-pass clock" % (100.0 * rc_clk / max(1, leaf_clk), 100.0 * ret_clk / max(1, leaf_clk)))
     reg = dbg[10:15].cpu().tolist()
     # split shading (no GS_FEAT_MIXED) stamps background / reconstruct / scatter on their own;
     # staged shading (GS_FEAT_MIXED, media, nested) stamps all of it as region 2
