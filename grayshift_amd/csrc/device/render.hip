@@ -824,8 +824,10 @@ __device__ GS_NOINLINE HitRec reconstruct(const DevScene& sc, Ray r, double t, u
     return h;
 }
 
-// The same for a hit that can only be a stationary sphere with a material that needs no uv
-// (GS_FEAT_PLAIN): reconstruct's sphere branch and HitRecord::new, nothing else.
+// The same for a hit that can only be a stationary sphere outside any instance (sphere-only
+// trees, GS_FEAT_SPHLEAF): reconstruct's sphere branch and HitRecord::new, nothing else; UV
+// false when no material needs uv (GS_FEAT_PLAIN).
+template <bool UV>
 __device__ __forceinline__ HitRec reconstruct_sphere(const DevScene& sc, const Ray& r, double t, uint32_t hit_ref) {
     HitRec h;
     const uint32_t idx = hit_ref & GS_REF_MASK;
@@ -834,11 +836,12 @@ __device__ __forceinline__ HitRec reconstruct_sphere(const DevScene& sc, const R
     h.mat = sc.sphere_mat[idx];
     const d3 p = add(r.o, muls(r.d, t));
     const d3 outward = divs(sub(p, c), s.r);
+    h.u = 0.0;
+    h.v = 0.0;
+    if (UV && sc.mats[h.mat].needs_uv) sphere_uv(outward, h.u, h.v);
     h.front = dot(r.d, outward) < 0.0;  // hittable.rs:26-43
     h.n = h.front ? outward : neg(outward);
     h.p = p;
-    h.u = 0.0;
-    h.v = 0.0;
     return h;
 }
 
@@ -930,7 +933,7 @@ struct ShadeOut {
 // in the same order; only which lanes issue an instruction together changes.
 // A hit lane's ray.o becomes the hit point p (the next ray's origin) as soon as p is
 // known: nothing after the HitRecord reads the old origin, and p need not stay live.
-template <bool PLAIN>
+template <bool PLAIN, bool SPH>
 __device__ __forceinline__ ShadeOut shade(const DevScene& sc, Ray& ray, double t, uint32_t hit_ref,
                                           uint32_t hit_inst, uint64_t& rng, unsigned long long* cnt) {
     const double PI = 3.14159265358979323846;
@@ -947,7 +950,8 @@ __device__ __forceinline__ ShadeOut shade(const DevScene& sc, Ray& ray, double t
     const DMaterial* m = sc.mats;
     if (!miss) {
         atomicAdd(&cnt[C_HITS], 1ull);
-        h = PLAIN ? reconstruct_sphere(sc, ray, t, hit_ref) : reconstruct(sc, ray, t, hit_ref, hit_inst);
+        h = PLAIN ? reconstruct_sphere<false>(sc, ray, t, hit_ref)
+            : SPH ? reconstruct_sphere<true>(sc, ray, t, hit_ref) : reconstruct(sc, ray, t, hit_ref, hit_inst);
         m = &sc.mats[h.mat];
         kind = m->kind;
         ray.o = h.p;
@@ -2217,12 +2221,12 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     uint64_t g2 = rng;
                     double c2 = closest;
                     asm volatile("" : "+v"(r2.d.x), "+v"(c2));
-                    const ShadeOut s2 = shade<(FEAT & GS_FEAT_PLAIN) != 0>(sc, r2, c2, hit_ref, LI(L_HINST), g2, s_cnt);
+                    const ShadeOut s2 = shade<(FEAT & GS_FEAT_PLAIN) != 0, kSphLeaf>(sc, r2, c2, hit_ref, LI(L_HINST), g2, s_cnt);
                     asm volatile("" ::"v"(s2.col.x), "v"(s2.col.y), "v"(s2.col.z), "v"(s2.dir.x), "v"(s2.dir.y), "v"(s2.dir.z),
                                  "v"(r2.o.x), "v"(g2), "v"(s2.cont));
                 }
 #endif
-                const ShadeOut s = shade<(FEAT & GS_FEAT_PLAIN) != 0>(sc, ray, closest, hit_ref,
+                const ShadeOut s = shade<(FEAT & GS_FEAT_PLAIN) != 0, kSphLeaf>(sc, ray, closest, hit_ref,
                                                                       (FEAT & GS_FEAT_PLAIN) ? GS_REF_NONE : LI(L_HINST), rng, s_cnt);
                 GS_MARK("shade_end");
                 GS_REGION(2, r0);
@@ -2256,7 +2260,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 } else {
                     atomicAdd(&s_cnt[C_HITS], 1ull);
                     GS_STAMP(r0);
-                    const HitRec h = reconstruct(sc, ray, closest, hit_ref, LI(L_HINST));
+                    const HitRec h = kSphLeaf ? reconstruct_sphere<true>(sc, ray, closest, hit_ref)
+                                              : reconstruct(sc, ray, closest, hit_ref, LI(L_HINST));
                     GS_REGION(1, r0);
                     GS_STAMP(r0);
                     const Scatter s = scatter(sc, h, ray.d, rng, s_cnt);
@@ -3709,7 +3714,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
         const int cases = (int)lamb + (int)metal + (int)diel + (int)iso + (int)(s->background.kind != GS_BG_SOLID);
         if (cases >= 3 && !(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED))) ds->feat |= GS_FEAT_MIXED;
     }
-    if (sph_leaves && leaf_runs && !(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED))) ds->feat |= GS_FEAT_SPHLEAF;
+    // (round 6: also without leaf runs -- C1, C2, A1's lone sphere -- for the sphere-only hit record)
+    if (sph_leaves && !(ds->feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED))) ds->feat |= GS_FEAT_SPHLEAF;
     if ((ds->feat & (GS_FEAT_SPHLEAF | GS_FEAT_MIXED)) == (GS_FEAT_SPHLEAF | GS_FEAT_MIXED) && g_plain_kernels) {
         // every hit a stationary sphere (SPHLEAF): plain materials, no uv -> GS_FEAT_PLAIN
         bool plain = true;
@@ -3849,6 +3855,12 @@ static void (*kernel_for(int feat))(KArgs) {
         GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_LDSTREE)
         GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_PLAIN)
         GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_PLAIN | GS_FEAT_LDSTREE)
+        GS_K(GS_FEAT_SPHLEAF)
+        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LDSTREE)
+        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_MIXED)
+        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_MIXED | GS_FEAT_LDSTREE)
+        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_MIXED | GS_FEAT_PLAIN)
+        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_MIXED | GS_FEAT_PLAIN | GS_FEAT_LDSTREE)
         case GS_FEAT_FIXED: return gs_render_kernel<GS_FEAT_FIXED>;
         case GS_FEAT_PILOT: return gs_render_kernel<GS_FEAT_PILOT>;
         default: return gs_render_kernel<0>;
