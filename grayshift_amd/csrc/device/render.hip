@@ -351,6 +351,14 @@ __device__ __forceinline__ d3 inv_cert(d3 d) {
     asm volatile("" : "+v"(d.x), "+v"(d.y), "+v"(d.z));  // (as inv_of: not hoisted)
     return mk(rcp_cert(d.x), rcp_cert(d.y), rcp_cert(d.z));
 }
+// Chunk sums and per-sample colours (written once, read by the combine kernel).  (Non-temporal
+// stores measured neutral, C4 +0.2%, final_scene +0.7%, and wrote as many fabric bytes: gfx950
+// stores leave L2 whatever their flavour, MI355X_MICROARCH.md; profiles/r06/ab_nt_partial.txt.)
+__device__ __forceinline__ void st_partial(double* o, double r, double g, double b) {
+    o[0] = r;
+    o[1] = g;
+    o[2] = b;
+}
 // A leaf record: the sphere's centre and radius squared, its next link and its ABI ref.
 template <bool LDS_ONLY>
 __device__ __forceinline__ void load_tleaf(const uint8_t* s_leaves, const TLeaf* g, uint32_t i, uint32_t lds_l,
@@ -1386,9 +1394,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     auto add_sample = [&](double Lr, double Lg, double Lb) {
         if (!kFixed && P->per_sample) {  // batch rounds: the sample's colour, summed in order by the combine
             double* o = P->partial + (size_t)LI(L_ITEM) * 3;
-            o[0] = Lr;
-            o[1] = Lg;
-            o[2] = Lb;
+            st_partial(o, Lr, Lg, Lb);
             LI(L_ITEM) += P->seg_n;
         } else {
             LD(L_CSR) += Lr;
@@ -1427,9 +1433,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
         const uint32_t item = LI(L_ITEM);
         if (kFixed || !P->per_sample) {
             double* o = P->partial + (size_t)item * 3;
-            o[0] = LD(L_CSR);
-            o[1] = LD(L_CSG);
-            o[2] = LD(L_CSB);
+            st_partial(o, LD(L_CSR), LD(L_CSG), LD(L_CSB));
         }
 #if !defined(GS_STAMPS) && !defined(GS_CERT_CHECK)  // (those builds use item_visits as their record buffer)
         if (P->item_visits) {  // (the item's packed pixel, from its chunk-major sum slot)
