@@ -323,6 +323,30 @@ __device__ __forceinline__ bool sphere_root_take(double h, double disc, double a
     return true;
 }
 
+// The same roots with the divisions by a taken from a refined reciprocal ra = rcp_cert(a)
+// (round 6): q = num ra, r = fma(-a, q, num), fma(r, ra, q) is the f64 division's own sequence
+// (v_div_scale, v_rcp, two Newton steps, v_div_fmas, v_div_fixup) with its scalings the
+// identity -- which they are for a in [2^-900, 2^900] and every numerator |num| >= 2^-968 (the
+// caller's condition on a; a smaller numerator gives |t| < 2^-68 < tmin, rejected either way,
+// and an overflowing one a NaN or infinity, rejected either way).  So every root inside
+// (tmin, tmax) is the correctly rounded quotient, bit for bit (test_gpu_device_kat.py).
+__device__ __forceinline__ double div_by(double num, double den, double rden) {
+    const double q = num * rden;
+    const double r = __builtin_fma(-den, q, num);
+    return __builtin_fma(r, rden, q);
+}
+__device__ __forceinline__ bool sphere_root_take_ra(double h, double disc, double a, double ra, double tmin, double tmax,
+                                                    double& t_out) {
+    double sq = sqrt(disc);
+    double t = div_by(h - sq, a, ra);
+    if (!(tmin < t && t < tmax)) {
+        t = div_by(h + sq, a, ra);
+        if (!(tmin < t && t < tmax)) return false;
+    }
+    t_out = t;
+    return true;
+}
+
 // HDRI::sample's texel column and row (camera.rs:257-270) for the rotated, normalised
 // direction `rot`: u = 0.5 + atan2(y, x) / 2pi, v = 0.5 - asin(z) / pi, then
 // `(u * W) as usize % W`, `(v * H) as usize % H`.  sky_index_f64 is that, in f64.

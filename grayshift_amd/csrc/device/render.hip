@@ -2058,15 +2058,27 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     const bool real1 = !(q1.disc < 0.0), real2 = two && !(q2.disc < 0.0);
                     GS_MARK("sphere_begin");
                     double t;
+                    // Root divisions by a from one refined reciprocal per pass (sphere_root_take_ra,
+                    // bit-identical for a in [2^-900, 2^900]: a wave-uniform choice, else `/`)
+#ifndef GS_ROOT_RCP
+#define GS_ROOT_RCP 1
+#endif
+                    const double ra = rcp_cert(a);
+                    const bool wave_ra =
+                        GS_ROOT_RCP && __builtin_amdgcn_ballot_w64(!(a >= 0x1p-900 && a <= 0x1p900)) == 0;
+                    auto take = [&](double hh, double dd) __attribute__((always_inline)) {
+                        return wave_ra ? sphere_root_take_ra(hh, dd, a, ra, tmin, closest, t)
+                                       : sphere_root_take(hh, dd, a, tmin, closest, t);
+                    };
                     if (real1 || real2) {
                         const double hA = real1 ? q1.h : q2.h, dA = real1 ? q1.disc : q2.disc;
-                        if (sphere_root_take(hA, dA, a, tmin, closest, t)) {
+                        if (take(hA, dA)) {
                             closest = t;
                             hit_ref = real1 ? ref : ref2;
                         }
                     }
                     if (real1 && real2) {
-                        if (sphere_root_take(q2.h, q2.disc, a, tmin, closest, t)) {
+                        if (take(q2.h, q2.disc)) {
                             closest = t;
                             hit_ref = ref2;
                         }

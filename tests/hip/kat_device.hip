@@ -62,6 +62,14 @@ __global__ void k_rcp_cert(int n, const double* d, double* approx, double* exact
     exact[i] = 1.0 / d[i];
 }
 
+// div_by (the sphere roots' division through a refined reciprocal) next to the exact quotient.
+__global__ void k_div_by(int n, const double* num, const double* den, double* fast, double* exact) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fast[i] = div_by(num[i], den[i], rcp_cert(den[i]));
+    exact[i] = num[i] / den[i];
+}
+
 __global__ void k_sphere(int n, const double* sph, const double* ray, const double* iv, double* t, int* hit) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -191,6 +199,16 @@ int kat_rcp_cert(int n, const double* d, double* approx, double* exact) {
     back(approx, da, n);
     back(exact, de, n);
     (void)hipFree(dd);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
+int kat_div_by(int n, const double* num, const double* den, double* fast, double* exact) {
+    double *dn = dcopy(num, n), *dd = dcopy(den, n);
+    double *df = dcopy<double>(nullptr, n), *de = dcopy<double>(nullptr, n);
+    hipLaunchKernelGGL(k_div_by, grid(n), dim3(256), 0, 0, n, dn, dd, df, de);
+    back(fast, df, n);
+    back(exact, de, n);
+    (void)hipFree(dn); (void)hipFree(dd);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 

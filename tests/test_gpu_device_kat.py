@@ -24,7 +24,7 @@ def kat(built):
                     "kat_math": [C.c_int, C.c_int, P, P, P],
                     "kat_noise": [C.c_int, C.c_int, P, C.c_double, P, P],
                     "kat_sky": [C.c_int, C.c_uint32, C.c_uint32, P, P],
-                    "kat_rcp_cert": [C.c_int, P, P, P]}.items():
+                    "kat_rcp_cert": [C.c_int, P, P, P], "kat_div_by": [C.c_int, P, P, P, P]}.items():
         getattr(L, f).argtypes = args
         getattr(L, f).restype = C.c_int
     return L
@@ -273,3 +273,35 @@ def test_rcp_cert_within_the_certificates_bound(kat):
         # rejected with the approximate value too; at a bound either choice is sound (the f64 test)
         out = ~((np.abs(exact) <= 2e15) & (np.abs(exact) >= 0.5e-25))
         assert out[:8].sum() >= 6 and not ok(approx[out]).any()
+
+
+def test_root_division_through_the_reciprocal_is_exact(kat):
+    """div_by (geometry.hpp, round 6: the sphere roots' (h -+ sqrt(disc)) / a through a refined
+    reciprocal of a) equals the correctly rounded division bit for bit for every denominator in
+    [2^-900, 2^900] and numerator >= 2^-968 in magnitude, incl. mantissas at the edges (all ones,
+    powers of two), exact quotients and signed zeros' neighbours; a quotient under 2^-68 (below
+    tmin) or an overflow may differ, and is rejected by the root's interval test either way."""
+    rng = np.random.default_rng(11)
+    n = 600000
+    def draw(lo, hi, m):
+        x = rng.uniform(1.0, 2.0, m) * np.exp2(rng.integers(lo, hi, m)).astype(np.float64)
+        return np.where(rng.random(m) < 0.5, -x, x)
+    den = np.abs(draw(-900, 900, n))
+    num = draw(-968, 1000, n)
+    k = n // 6  # edge mantissas: 1.111...1 and exact powers of two, exact small-integer quotients
+    den[:k] = np.nextafter(np.exp2(rng.integers(-60, 60, k)).astype(np.float64), 0.0)
+    num[k:2 * k] = np.exp2(rng.integers(-60, 60, k)).astype(np.float64)
+    den[2 * k:3 * k] = rng.integers(1, 1 << 20, k).astype(np.float64)
+    num[2 * k:3 * k] = den[2 * k:3 * k] * rng.integers(-1000, 1000, k)
+    # the sphere's own shapes: a = |d|^2 of unit-ish directions, numerators h -+ sqrt(disc)
+    den[3 * k:4 * k] = rng.uniform(0.01, 100.0, k)
+    num[3 * k:4 * k] = rng.normal(scale=50.0, size=k)
+    num, den = np.ascontiguousarray(num), np.ascontiguousarray(den)
+    fast, exact = np.zeros(n), np.zeros(n)
+    assert kat.kat_div_by(n, ptr(num), ptr(den), ptr(fast), ptr(exact)) == 0
+    with np.errstate(all="ignore"):
+        q = np.abs(num / den)
+    inside = (q >= 2.0 ** -68) & np.isfinite(q) & (q < 1.7e308)
+    assert inside.sum() > n // 2
+    same = fast.view(np.uint64) == exact.view(np.uint64)
+    assert same[inside].all(), (num[inside & ~same][:4], den[inside & ~same][:4])
