@@ -347,6 +347,19 @@ __device__ __forceinline__ bool sphere_root_take_ra(double h, double disc, doubl
     return true;
 }
 
+// sphere_accept_rr with the roots' divisions through ra = rcp_cert(a) (the caller has checked a
+// is in [2^-900, 2^900] for every active lane: sphere_root_take_ra's condition)
+__device__ __forceinline__ bool sphere_accept_rr_ra(d3 c, double rr, const Ray& ray, double a, double ra, double tmin,
+                                                    double tmax, double& t_out) {
+    d3 oc = sub(c, ray.o);
+    double h = dot(ray.d, oc);
+    double cc = len2(oc) - rr;
+    double disc = h * h - a * cc;
+    t_out = tmax;
+    if (disc < 0.0) return false;
+    return sphere_root_take_ra(h, disc, a, ra, tmin, tmax, t_out);
+}
+
 // HDRI::sample's texel column and row (camera.rs:257-270) for the rotated, normalised
 // direction `rot`: u = 0.5 + atan2(y, x) / 2pi, v = 0.5 - asin(z) / pi, then
 // `(u * W) as usize % W`, `(v * H) as usize % H`.  sky_index_f64 is that, in f64.

@@ -79,6 +79,9 @@ using namespace gsd;
 #define GS_FEAT_VISITS 32 // count tests per threaded record (the placement pilot, run_pilot)
 #define GS_FEAT_SPHLEAF 64 // every top-level leaf is a stationary sphere (no media / nested BVHs):
                            // leaf passes without the other kinds' code or the kind test
+#ifndef GS_ROOT_RCP
+#define GS_ROOT_RCP 1  // sphere roots divided through a refined reciprocal of a (sphere_root_take_ra; A/B: 0)
+#endif
 #define GS_FEAT_PLAIN 256  // staged shading of sphere-only trees whose materials are all solid / two-solid
                            // checker Lambertians, metals and dielectrics with no uv: the hit record of a
                            // stationary sphere only, no texture, light or isotropic code (round 6; C4)
@@ -2021,11 +2024,23 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     dist_bad += bad && first;
                 }
 #endif
+                // a stationary sphere's test (sphere.rs:64-106); its root divisions through one
+                // refined reciprocal of a when every active lane's a is in range (as the
+                // sphere-only leaf runs below), else the f64 division
+                auto sphere_test = [&](d3 c, double rr, double& t) __attribute__((always_inline)) {
+                    const double a = len2(ray.d);
+                    // (not in media / nested-BVH kernels: final_scene and cornell_smoke measured
+                    // neutral, and the media kernel spilled 12 B/lane with it)
+                    constexpr bool kRa = GS_ROOT_RCP && (FEAT & (GS_FEAT_MEDIA | GS_FEAT_NESTED)) == 0;
+                    if (kRa && __builtin_amdgcn_ballot_w64(!(a >= 0x1p-900 && a <= 0x1p900)) == 0)
+                        return sphere_accept_rr_ra(c, rr, ray, a, rcp_cert(a), tmin, closest, t);
+                    return sphere_accept_rr(c, rr, ray, a, tmin, closest, t);
+                };
                 auto sphere_leaf = [&]() __attribute__((always_inline)) {  // a stationary sphere, inline
                     GS_MARK("sphere_begin");
                     count_sph();
                     double t;
-                    if (sphere_accept_rr(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
+                    if (sphere_test(mk(scx, scy, scz), sr, t)) {
                         closest = t;
                         closest32 = (float)t;
                         hit_ref = ref;
@@ -2060,9 +2075,6 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     double t;
                     // Root divisions by a from one refined reciprocal per pass (sphere_root_take_ra,
                     // bit-identical for a in [2^-900, 2^900]: a wave-uniform choice, else `/`)
-#ifndef GS_ROOT_RCP
-#define GS_ROOT_RCP 1
-#endif
                     const double ra = rcp_cert(a);
                     const bool wave_ra =
                         GS_ROOT_RCP && __builtin_amdgcn_ballot_w64(!(a >= 0x1p-900 && a <= 0x1p900)) == 0;
@@ -2167,7 +2179,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     }
                     count_sph();
                     double t;
-                    if (sphere_accept_rr(mk(scx, scy, scz), sr, ray, len2(ray.d), tmin, closest, t)) {
+                    if (sphere_test(mk(scx, scy, scz), sr, t)) {
                         closest = t;
                         closest32 = (float)t;
                         hit_ref = ref;
