@@ -60,7 +60,10 @@ using namespace gsd;
 #ifndef GS_MIN_WAVES
 #define GS_MIN_WAVES 4
 #endif
-#define GS_MAX_CHAIN 4
+// The longest Translate / RotateY chain (instances in a row, an outer chain -- a BVH's -- and an
+// inner one -- a leaf's inside that BVH -- counted together; round 6: was 4).  reconstruct keeps
+// the first 4 in registers and re-walks deeper ones.
+#define GS_MAX_CHAIN 16
 // Batch rounds (adaptive settings): whole-batch items only for batches up to this size
 #ifndef GS_ROUND_WHOLE_MAX_BATCH
 #define GS_ROUND_WHOLE_MAX_BATCH 256
@@ -762,15 +765,37 @@ __device__ __forceinline__ void sphere_uv(d3 p, double& u, double& v) {  // sphe
 
 // Recompute the HitRecord of the accepted primitive at t (the values the reference
 // built when it accepted it), then apply the instance back-transforms innermost-first.
+// hit_inst: the chain the hit came through (GS_REF_NONE: none); outer: for a hit through a
+// chain inside a BVH that is itself under a chain (round 6), that BVH's chain (applied first
+// going in, last coming out), else GS_REF_NONE.
+// The n-th instance of the concatenated chain (outer's, then hit_inst's).
+__device__ __forceinline__ uint32_t chain_at(const DevScene& sc, uint32_t outer, uint32_t inner, int n) {
+    uint32_t cur = outer != GS_REF_NONE ? outer : inner;
+    bool in_outer = outer != GS_REF_NONE;
+#pragma unroll 1
+    for (int k = 0; k < 2 * GS_MAX_CHAIN; k++) {
+        if ((cur >> GS_REF_SHIFT) != GS_REF_INSTANCE) {  // the outer chain ended: the inner one
+            if (!in_outer) break;
+            in_outer = false;
+            cur = inner;
+            k--;
+            continue;
+        }
+        if (n-- == 0) return cur & GS_REF_MASK;
+        cur = sc.inst[cur & GS_REF_MASK].child;
+    }
+    return 0u;
+}
 __device__ GS_NOINLINE HitRec reconstruct(const DevScene& sc, Ray r, double t, uint32_t hit_ref,
-                                           uint32_t hit_inst) {
+                                           uint32_t hit_inst, uint32_t outer = GS_REF_NONE) {
     HitRec h;
     uint32_t ch0 = 0, ch1 = 0, ch2 = 0, ch3 = 0;
     int nch = 0;
-    if (hit_inst != GS_REF_NONE) {
+    bool deep = outer != GS_REF_NONE;  // two chains, or one longer than 4: the re-walking path
+    if (hit_inst != GS_REF_NONE && !deep) {
         uint32_t cur = hit_inst;
 #pragma unroll
-        for (int k = 0; k < GS_MAX_CHAIN; k++) {
+        for (int k = 0; k < 4; k++) {
             if ((cur >> GS_REF_SHIFT) != GS_REF_INSTANCE) break;
             uint32_t i = cur & GS_REF_MASK;
             if (k == 0) ch0 = i; else if (k == 1) ch1 = i; else if (k == 2) ch2 = i; else ch3 = i;
@@ -778,6 +803,32 @@ __device__ GS_NOINLINE HitRec reconstruct(const DevScene& sc, Ray r, double t, u
             const gs_instance& in = sc.inst[i];
             inst_forward(in, r);
             cur = in.child;
+        }
+        if ((cur >> GS_REF_SHIFT) == GS_REF_INSTANCE) {  // deeper than 4: on through the rest
+            deep = true;
+#pragma unroll 1
+            for (int k = 4; k < GS_MAX_CHAIN && (cur >> GS_REF_SHIFT) == GS_REF_INSTANCE; k++) {
+                const gs_instance& in = sc.inst[cur & GS_REF_MASK];
+                inst_forward(in, r);
+                cur = in.child;
+                nch = k + 1;
+            }
+        }
+    } else if (deep) {  // the outer chain, then the inner one
+        uint32_t cur = outer;
+        bool in_outer = true;
+#pragma unroll 1
+        for (int k = 0; k < 2 * GS_MAX_CHAIN; k++) {
+            if ((cur >> GS_REF_SHIFT) != GS_REF_INSTANCE) {
+                if (!in_outer || hit_inst == GS_REF_NONE) break;
+                in_outer = false;
+                cur = hit_inst;
+                continue;
+            }
+            const gs_instance& in = sc.inst[cur & GS_REF_MASK];
+            inst_forward(in, r);
+            cur = in.child;
+            nch++;
         }
     }
     const uint32_t kind = hit_ref >> GS_REF_SHIFT, idx = hit_ref & GS_REF_MASK;
@@ -824,10 +875,15 @@ __device__ GS_NOINLINE HitRec reconstruct(const DevScene& sc, Ray r, double t, u
     h.front = dot(r.d, outward) < 0.0;
     d3 n = h.front ? outward : neg(outward);
     // Innermost instance first (RotateY inside Translate: rotate back, then translate).
-    if (nch > 3) inst_backward(sc.inst[ch3], p, n);
-    if (nch > 2) inst_backward(sc.inst[ch2], p, n);
-    if (nch > 1) inst_backward(sc.inst[ch1], p, n);
-    if (nch > 0) inst_backward(sc.inst[ch0], p, n);
+    if (!deep) {
+        if (nch > 3) inst_backward(sc.inst[ch3], p, n);
+        if (nch > 2) inst_backward(sc.inst[ch2], p, n);
+        if (nch > 1) inst_backward(sc.inst[ch1], p, n);
+        if (nch > 0) inst_backward(sc.inst[ch0], p, n);
+    } else {
+#pragma unroll 1
+        for (int k = nch - 1; k >= 0; k--) inst_backward(sc.inst[chain_at(sc, outer, hit_inst, k)], p, n);
+    }
     h.p = p;
     h.n = n;
     h.u = u;
@@ -946,7 +1002,8 @@ struct ShadeOut {
 // known: nothing after the HitRecord reads the old origin, and p need not stay live.
 template <bool PLAIN, bool SPH>
 __device__ __forceinline__ ShadeOut shade(const DevScene& sc, Ray& ray, double t, uint32_t hit_ref,
-                                          uint32_t hit_inst, uint64_t& rng, unsigned long long* cnt) {
+                                          uint32_t hit_inst, uint64_t& rng, unsigned long long* cnt,
+                                          uint32_t hit_outer = GS_REF_NONE) {
     const double PI = 3.14159265358979323846;
     ShadeOut o;
     o.cont = 0;
@@ -962,7 +1019,7 @@ __device__ __forceinline__ ShadeOut shade(const DevScene& sc, Ray& ray, double t
     if (!miss) {
         atomicAdd(&cnt[C_HITS], 1ull);
         h = PLAIN ? reconstruct_sphere<false>(sc, ray, t, hit_ref)
-            : SPH ? reconstruct_sphere<true>(sc, ray, t, hit_ref) : reconstruct(sc, ray, t, hit_ref, hit_inst);
+            : SPH ? reconstruct_sphere<true>(sc, ray, t, hit_ref) : reconstruct(sc, ray, t, hit_ref, hit_inst, hit_outer);
         m = &sc.mats[h.mat];
         kind = m->kind;
         ray.o = h.p;
@@ -2132,9 +2189,20 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         closest = lh.t;
                         closest32 = (float)lh.t;
                         hit_ref = lh.ref;
-                        // (a primitive or list in the tree under LNINST; an instance leaf's own chain)
-                        if constexpr (kNested) LI(L_HINST) = lh.inst != GS_REF_NONE ? lh.inst : LNINST;
-                        else LI(L_HINST) = lh.inst;
+                        // (a primitive or list in the tree under LNINST; an instance leaf's own chain;
+                        // round 6: an instance leaf inside the tree under LNINST -- both chains, the
+                        // outer one in the save slot, bit 31 on the inner one)
+                        if constexpr (kNested) {
+                            if (lh.inst != GS_REF_NONE && LNINST != GS_REF_NONE) {
+                                P->nest_save[((size_t)blockIdx.x * GS_BLOCK + tid) * 8u + 7u] =
+                                    __longlong_as_double((long long)LNINST);
+                                LI(L_HINST) = lh.inst | 0x80000000u;
+                            } else {
+                                LI(L_HINST) = lh.inst != GS_REF_NONE ? lh.inst : LNINST;
+                            }
+                        } else {
+                            LI(L_HINST) = lh.inst;
+                        }
                     }
                     if constexpr (kNested) {
                         // The chain ended in a BVH (final_scene's box of balls): the lane walks
@@ -2254,8 +2322,17 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                                  "v"(r2.o.x), "v"(g2), "v"(s2.cont));
                 }
 #endif
-                const ShadeOut s = shade<(FEAT & GS_FEAT_PLAIN) != 0, kSphLeaf>(sc, ray, closest, hit_ref,
-                                                                      (FEAT & GS_FEAT_PLAIN) ? GS_REF_NONE : LI(L_HINST), rng, s_cnt);
+                // (GS_FEAT_NESTED: a hit through a chain inside a BVH under another chain carries
+                // bit 31 on its inner chain's ref, the outer chain in the lane's save slot 7)
+                uint32_t hinst = (FEAT & GS_FEAT_PLAIN) ? GS_REF_NONE : LI(L_HINST), houter = GS_REF_NONE;
+                if constexpr (kNested) {
+                    if (hinst != GS_REF_NONE && (hinst >> 31)) {
+                        houter = (uint32_t)__double_as_longlong(P->nest_save[((size_t)blockIdx.x * GS_BLOCK + tid) * 8u + 7u]);
+                        hinst &= 0x7FFFFFFFu;
+                    }
+                }
+                const ShadeOut s = shade<(FEAT & GS_FEAT_PLAIN) != 0, kSphLeaf>(sc, ray, closest, hit_ref, hinst, rng, s_cnt,
+                                                                              houter);
                 GS_MARK("shade_end");
                 GS_REGION(2, r0);
                 if (s.cont) {
@@ -3084,8 +3161,14 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
                 if (s.nodes[i].right != GS_REF_NONE) st.push_back({s.nodes[i].right, d + 1});
             } else {
                 // (since round 5 the tree is walked by the main passes, whose leaf test takes
-                // media like the top level's: the hit's instance is the tree's chain)
-                const int e = (r >> GS_REF_SHIFT) == GS_REF_MEDIUM ? medium_ok(r) : shape_ok(r);
+                // media like the top level's: the hit's instance is the tree's chain; round 6: a
+                // chain inside the tree, ending in a primitive, list or medium -- not another BVH)
+                uint32_t c = r;
+                int e = chain_ok(c);
+                if (!e) {
+                    if ((c >> GS_REF_SHIFT) == GS_REF_NODE) e = 2;
+                    else e = (c >> GS_REF_SHIFT) == GS_REF_MEDIUM ? medium_ok(c) : shape_ok(c);
+                }
                 if (e) return e;
             }
         }
@@ -3121,10 +3204,10 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
         } else {
             int e = leaf_ok(r);
             if (e == 1) return bad("leaf reference");
-            if (e == 2) return unsup("instance chain deeper than 4, a BVH under an instance deeper than " +
-                                     std::to_string(GS_NESTED_STACK) + " or with leaves that are not lists, "
-                                     "primitives or media, a BVH inside a medium boundary, nested media, or a list "
-                                     "member that is not a primitive");
+            if (e == 2) return unsup("instance chain deeper than " + std::to_string(GS_MAX_CHAIN) +
+                                     ", a BVH under an instance deeper than " + std::to_string(GS_NESTED_STACK) +
+                                     " or holding another BVH under an instance, a BVH inside a medium boundary, "
+                                     "nested media, or a list member that is not a primitive");
         }
     }
     *depth_out = maxd;

@@ -342,13 +342,14 @@ uint32_t HittableList::flatten(Flattener& f) const {
     return GS_MAKE_REF(GS_REF_LIST, f.lists.size() - 1);
 }
 static uint32_t flatten_instance_child(Flattener& f, const Hittable& o) {
-    if (f.inside_nested_bvh)
-        throw std::domain_error("Translate/RotateY inside a BVH that is itself under Translate/RotateY is not "
-                                "supported on the device path");
-    bool was = f.inside_instance;
+    // (round 6: a chain inside a BVH that is itself under a chain is accepted -- the device keeps
+    // both chains of such a hit -- but not a further BVH under it, BVHNode::flatten)
+    bool was = f.inside_instance, was_in = f.instance_in_nested;
     f.inside_instance = true;
+    if (f.inside_nested_bvh) f.instance_in_nested = true;
     uint32_t r = o.flatten(f);
     f.inside_instance = was;
+    f.instance_in_nested = was_in;
     return r;
 }
 uint32_t Translate::flatten(Flattener& f) const {
@@ -378,6 +379,9 @@ uint32_t RotateY::flatten(Flattener& f) const {
 }
 uint32_t BVHNode::flatten(Flattener& f) const {
     if (f.inside_medium) throw std::domain_error("BVH as a ConstantMedium boundary is not supported on the device path");
+    if (f.instance_in_nested)
+        throw std::domain_error("a BVH under Translate/RotateY inside a BVH that is itself under Translate/RotateY "
+                                "(two levels of nested BVHs) is not supported on the device path");
     // A BVH under Translate/RotateY (final_scene's balls, main.rs:741-755) is walked by the
     // device as a second-level tree on its own stack: its depth does not count towards
     // the top-level (LDS) stack.

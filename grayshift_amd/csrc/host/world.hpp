@@ -343,6 +343,7 @@ public:
     bool inside_instance = false;
     bool inside_medium = false;  // flattening a ConstantMedium boundary
     bool inside_nested_bvh = false;  // flattening a BVH under Translate/RotateY
+    bool instance_in_nested = false;  // flattening a Translate/RotateY inside such a BVH (round 6)
 };
 
 // A flattened world + background, ready for gs_render / gs_device_scene_create.

@@ -231,20 +231,25 @@ def test_bvh_under_instance_flattens_as_a_second_level_tree():
     hs.close()
 
 
-@pytest.mark.parametrize("case", ["instance_in_nested", "medium_in_nested"])
+@pytest.mark.parametrize("case", ["instance_in_nested", "medium_in_nested", "bvh_in_instance_in_nested"])
 def test_nested_bvh_leaves(case):
-    """A Translate/RotateY chain inside a BVH that is itself under one stays unsupported (a hit
-    would need two chains composed); a ConstantMedium there is accepted since round 5 (the
-    device walks such trees in its main passes; GPU parity: test_gpu_volumes.py)."""
+    """A ConstantMedium inside a BVH that is itself under Translate/RotateY is accepted since
+    round 5, a Translate/RotateY chain there since round 6 (the device keeps both chains of
+    such a hit; GPU parity: test_gpu_composition.py); a further BVH under that chain (two
+    levels of nested BVHs) stays unsupported."""
     b = SceneBuilder()
     m = b.lambertian((1, 1, 1))
     s1 = b.sphere((0, 0, 0), 1, m)
-    odd = b.translate(b.sphere((3, 0, 0), 1, m), (0, 1, 0)) if case == "instance_in_nested" else \
-        b.medium(b.sphere((3, 0, 0), 1, m), 0.5, b.isotropic((1, 1, 1)))
+    if case == "instance_in_nested":
+        odd = b.translate(b.sphere((3, 0, 0), 1, m), (0, 1, 0))
+    elif case == "medium_in_nested":
+        odd = b.medium(b.sphere((3, 0, 0), 1, m), 0.5, b.isotropic((1, 1, 1)))
+    else:
+        odd = b.translate(b.bvh([b.sphere((3, 0, 0), 1, m), b.sphere((3, 3, 0), 1, m)]), (0, 1, 0))
     b.add(b.translate(b.bvh([s1, odd, b.sphere((6, 0, 0), 1, m)]), (1, 0, 0)))
     h = C.c_void_p()
     rc = N.lib.gs_host_scene_from_spec(b.build().ptr(), C.byref(h))
-    if case == "instance_in_nested":
+    if case == "bvh_in_instance_in_nested":
         assert rc == N.GS_ERR_UNSUPPORTED
     else:
         assert rc == N.GS_OK
