@@ -32,6 +32,7 @@
 #include <cstring>
 #include <atomic>
 #include <chrono>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -85,6 +86,11 @@ using namespace gsd;
 #ifndef GS_ROOT_RCP
 #define GS_ROOT_RCP 1  // sphere roots divided through a refined reciprocal of a (sphere_root_take_ra; A/B: 0)
 #endif
+#define GS_FEAT_GENERAL 512 // compositions beyond the reference scenes' (round 6): Translate / RotateY chains
+                            // deeper than 4, chains inside a BVH under a chain (two-chain hit records), a BVH
+                            // as a ConstantMedium boundary, a medium as a medium's boundary.  One catch-all
+                            // instantiation (with media, nested BVHs, leaf runs, staged shading); the other
+                            // kernels keep the 4-deep single-chain hit record
 #define GS_FEAT_PLAIN 256  // staged shading of sphere-only trees whose materials are all solid / two-solid
                            // checker Lambertians, metals and dielectrics with no uv: the hit record of a
                            // stationary sphere only, no texture, light or isotropic code (round 6; C4)
@@ -97,6 +103,7 @@ using namespace gsd;
 __host__ __device__ constexpr int unroll_steps(int feat) { return GS_NODE_STEPS; }
 // The pilot's instantiation: every code path (any scene), plus the counts.
 #define GS_FEAT_PILOT (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_VISITS)
+#define GS_FEAT_GENERAL_KERNEL (GS_FEAT_GENERAL | GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_LEAFRUN | GS_FEAT_MIXED)
 
 // ---------------------------------------------------------------- device layout
 // Internal layouts (may differ from the ABI records; converted at upload).
@@ -161,6 +168,11 @@ struct DevScene {
     const uint32_t* hdri_rgbe;  // non-null when every texel round-trips through RGBE8
     gs_background bg;
     uint32_t root;
+    // the threaded records (GS_FEAT_GENERAL: a BVH as a medium boundary is walked from global
+    // memory by tree_test; the kernels' own walks read them through KArgs and the LDS mirror)
+    const TNode* tnodes;
+    const TBox* tboxes;
+    const TLeaf* tleaves;
 };
 
 // Cold launch parameters: written to device memory per launch and read through a
@@ -239,7 +251,8 @@ struct KParams {
     uint32_t* round_counts;    // [rounds + 1]: active pixels per round
     double* pstate;            // per packed pixel: the running Σr, Σg, Σb, Σlum, Σlum² (camera.rs:131-146)
     // GS_FEAT_NESTED: per lane (block * GS_BLOCK + thread), the top-level ray while the lane
-    // walks a BVH under an instance chain: o, d (6 doubles), then the return link (u32)
+    // walks a BVH under an instance chain: o, d (6 doubles), the return link (u32), and (the
+    // general kernel) a hit's outer chain -- slot k of lane g at [k * grid lanes + g]
     double* nest_save;
 };
 
@@ -261,7 +274,8 @@ struct KArgs {
     uint32_t lds_quads;  // then quad records [0, lds_quads)
     uint32_t lds_cubes;  // then the Quad::cube records [0, lds_cubes) (cube_test)
     const double* cubes; // (the mirror's source)
-    uint32_t lane_nd;    // f64 lane-state fields in LDS: lane_nd(chunked)
+    uint32_t lane_nd;    // f64 lane-state fields in LDS: lane_nd(chunked) + nest_lds
+    uint32_t nest_lds;   // of which the nested walk's save slots (0: in KParams::nest_save)
 };
 
 // S_CAM: the lane's next sample needs its camera ray (set by the refill for a new item and
@@ -671,13 +685,58 @@ __device__ __forceinline__ void shape_test(const DevScene& sc, const QuadSrc& qs
     }
 }
 
+// GS_FEAT_GENERAL: the closest hit of `r` over BVH tree `tree` (threaded like the BVHs under
+// instances, its last links THR_RET) in [tmin, res.t] -- BVHNode::hit (BVH.rs:69-90) as its
+// pre-order walk with the shrinking closest, every node tested with the reference's f64 slab
+// test (AABB.rs:58-113) and counted, the leaves' lists and primitives by shape_test.  For a
+// BVH as a ConstantMedium boundary: a rare path, read from global memory.
+template <bool UNI>
+__device__ __forceinline__ void tree_test(const DevScene& sc, const QuadSrc& qs, uint32_t tree, const Ray& r, double tmin,
+                                          LeafHit& res, unsigned long long* cnt) {
+    uint32_t link = sc.nroots[tree];
+    const d3 inv = inv_of(r.d);
+#pragma unroll 1
+    for (uint32_t guard = 0; link != THR_RET && guard < (1u << 27); guard++) {
+        if (link < THR_END) {  // a node record (its byte offset)
+            atomicAdd(&cnt[C_NODES], 1ull);
+            const TNode& n = sc.tnodes[link >> 5];
+            link = box_hit(box64(sc.tboxes[link >> 5]), r.o, inv, tmin, res.t) ? n.hit : n.miss;
+        } else {  // a leaf record
+            const TLeaf& lf = sc.tleaves[link & ~THR_LEAF];
+            shape_test<false>(sc, qs, lf.ref, r, tmin, res.t, GS_REF_NONE, res, cnt);
+            link = lf.next;
+        }
+    }
+}
+
+template <bool UNI, int LEVEL>
+__device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& qs, uint32_t cur, const Ray& r, double tmin,
+                                            double closest, uint32_t inst_ref, uint64_t& rng, LeafHit& res,
+                                            unsigned long long* cnt, bool general);
+// A medium's boundary in [tmin, DMAX]: a primitive or list; with GS_FEAT_GENERAL also a BVH
+// (tree_test) or, one level deep, another medium (its own ConstantMedium::hit, drawing from
+// the lane's stream in the reference's order: volume.rs:36-41 calls boundary.hit twice).
+template <bool UNI, int LEVEL>
+__device__ __forceinline__ void boundary_test(const DevScene& sc, const QuadSrc& qs, uint32_t shape, const Ray& rb,
+                                              double tmin, uint64_t& rng, LeafHit& b, unsigned long long* cnt,
+                                              bool general) {
+    if (general && (shape >> GS_REF_SHIFT) == GS_REF_NODE) {
+        tree_test<UNI>(sc, qs, shape & GS_REF_MASK, rb, tmin, b, cnt);
+    } else if (LEVEL == 0 && general && (shape >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
+        medium_test<false, 1>(sc, qs, shape, rb, tmin, b.t, GS_REF_NONE, rng, b, cnt, true);
+    } else {
+        shape_test<UNI>(sc, qs, shape, rb, tmin, b.t, GS_REF_NONE, b, cnt);
+    }
+}
+
 // ConstantMedium::hit (volume.rs:32-63): the boundary hit over Interval::UNIVERSE, again
 // from t1 + 0.0001, both clipped to ray_t; then the free-flight distance from the lane's
 // RNG stream, drawn here, inside traversal, in the reference's visit order (:48).
-template <bool UNI>
+// `general` (GS_FEAT_GENERAL kernels): the boundary may be a BVH or a medium (boundary_test).
+template <bool UNI, int LEVEL>
 __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& qs, uint32_t cur, const Ray& r, double tmin,
                                             double closest, uint32_t inst_ref, uint64_t& rng, LeafHit& res,
-                                            unsigned long long* cnt) {
+                                            unsigned long long* cnt, bool general) {
     atomicAdd(&cnt[C_MED], 1ull);
     // the boundary now, the density only where it is used (not held through both hits)
     const gs_medium* mp = sc.media + (cur & GS_REF_MASK);
@@ -697,13 +756,15 @@ __device__ __forceinline__ void medium_test(const DevScene& sc, const QuadSrc& q
     b1.t = DMAX;
     Ray rb = r;
     const uint32_t shape = walk_chain<UNI>(sc, md.boundary, rb, cnt);
-    shape_test<UNI>(sc, qs, shape, rb, -DMAX, DMAX, GS_REF_NONE, b1, cnt);
+    if (general) boundary_test<UNI, LEVEL>(sc, qs, shape, rb, -DMAX, rng, b1, cnt, true);
+    else shape_test<UNI>(sc, qs, shape, rb, -DMAX, DMAX, GS_REF_NONE, b1, cnt);
     if (!b1.hit) return;
     chain_count<UNI>(sc, md.boundary, cnt);
     LeafHit b2;
     b2.hit = false;
     b2.t = DMAX;
-    shape_test<UNI>(sc, qs, shape, rb, b1.t + 0.0001, DMAX, GS_REF_NONE, b2, cnt);
+    if (general) boundary_test<UNI, LEVEL>(sc, qs, shape, rb, b1.t + 0.0001, rng, b2, cnt, true);
+    else shape_test<UNI>(sc, qs, shape, rb, b1.t + 0.0001, DMAX, GS_REF_NONE, b2, cnt);
     if (!b2.hit) return;
     double t1 = b1.t, t2 = b2.t;
     if (t1 < tmin) t1 = tmin;
@@ -739,7 +800,7 @@ __device__ GS_NOINLINE LeafHit leaf_other(const DevScene& sc, const QuadSrc& qs,
     const uint32_t inst_ref = (ref >> GS_REF_SHIFT) == GS_REF_INSTANCE ? ref : GS_REF_NONE;
     const uint32_t cur = walk_chain<UNI>(sc, ref, r, cnt);
     if ((FEAT & GS_FEAT_MEDIA) && (cur >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
-        medium_test<UNI>(sc, qs, cur, r, tmin, closest, inst_ref, rng, res, cnt);
+        medium_test<UNI, 0>(sc, qs, cur, r, tmin, closest, inst_ref, rng, res, cnt, (FEAT & GS_FEAT_GENERAL) != 0);
     } else if ((FEAT & GS_FEAT_NESTED) && (cur >> GS_REF_SHIFT) == GS_REF_NODE) {
         res.enter = (cur & GS_REF_MASK) + 1u;
     } else {
@@ -786,12 +847,13 @@ __device__ __forceinline__ uint32_t chain_at(const DevScene& sc, uint32_t outer,
     }
     return 0u;
 }
+template <bool DEEP>  // GS_FEAT_GENERAL kernels: chains longer than 4, two chains
 __device__ GS_NOINLINE HitRec reconstruct(const DevScene& sc, Ray r, double t, uint32_t hit_ref,
                                            uint32_t hit_inst, uint32_t outer = GS_REF_NONE) {
     HitRec h;
     uint32_t ch0 = 0, ch1 = 0, ch2 = 0, ch3 = 0;
     int nch = 0;
-    bool deep = outer != GS_REF_NONE;  // two chains, or one longer than 4: the re-walking path
+    bool deep = DEEP && outer != GS_REF_NONE;  // two chains, or one longer than 4: the re-walking path
     if (hit_inst != GS_REF_NONE && !deep) {
         uint32_t cur = hit_inst;
 #pragma unroll
@@ -804,7 +866,7 @@ __device__ GS_NOINLINE HitRec reconstruct(const DevScene& sc, Ray r, double t, u
             inst_forward(in, r);
             cur = in.child;
         }
-        if ((cur >> GS_REF_SHIFT) == GS_REF_INSTANCE) {  // deeper than 4: on through the rest
+        if (DEEP && (cur >> GS_REF_SHIFT) == GS_REF_INSTANCE) {  // deeper than 4: on through the rest
             deep = true;
 #pragma unroll 1
             for (int k = 4; k < GS_MAX_CHAIN && (cur >> GS_REF_SHIFT) == GS_REF_INSTANCE; k++) {
@@ -814,7 +876,7 @@ __device__ GS_NOINLINE HitRec reconstruct(const DevScene& sc, Ray r, double t, u
                 nch = k + 1;
             }
         }
-    } else if (deep) {  // the outer chain, then the inner one
+    } else if (DEEP && deep) {  // the outer chain, then the inner one
         uint32_t cur = outer;
         bool in_outer = true;
 #pragma unroll 1
@@ -875,7 +937,7 @@ __device__ GS_NOINLINE HitRec reconstruct(const DevScene& sc, Ray r, double t, u
     h.front = dot(r.d, outward) < 0.0;
     d3 n = h.front ? outward : neg(outward);
     // Innermost instance first (RotateY inside Translate: rotate back, then translate).
-    if (!deep) {
+    if (!DEEP || !deep) {
         if (nch > 3) inst_backward(sc.inst[ch3], p, n);
         if (nch > 2) inst_backward(sc.inst[ch2], p, n);
         if (nch > 1) inst_backward(sc.inst[ch1], p, n);
@@ -1000,7 +1062,7 @@ struct ShadeOut {
 // in the same order; only which lanes issue an instruction together changes.
 // A hit lane's ray.o becomes the hit point p (the next ray's origin) as soon as p is
 // known: nothing after the HitRecord reads the old origin, and p need not stay live.
-template <bool PLAIN, bool SPH>
+template <bool PLAIN, bool SPH, bool GEN>
 __device__ __forceinline__ ShadeOut shade(const DevScene& sc, Ray& ray, double t, uint32_t hit_ref,
                                           uint32_t hit_inst, uint64_t& rng, unsigned long long* cnt,
                                           uint32_t hit_outer = GS_REF_NONE) {
@@ -1019,7 +1081,7 @@ __device__ __forceinline__ ShadeOut shade(const DevScene& sc, Ray& ray, double t
     if (!miss) {
         atomicAdd(&cnt[C_HITS], 1ull);
         h = PLAIN ? reconstruct_sphere<false>(sc, ray, t, hit_ref)
-            : SPH ? reconstruct_sphere<true>(sc, ray, t, hit_ref) : reconstruct(sc, ray, t, hit_ref, hit_inst, hit_outer);
+            : SPH ? reconstruct_sphere<true>(sc, ray, t, hit_ref) : reconstruct<GEN>(sc, ray, t, hit_ref, hit_inst, hit_outer);
         m = &sc.mats[h.mat];
         kind = m->kind;
         ray.o = h.p;
@@ -1318,6 +1380,22 @@ enum { L_ND_CHUNKED = L_LSUM };
 __host__ __device__ constexpr bool t_in_lds(int feat) {
     return (feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED)) != 0 && (feat & GS_FEAT_VISITS) == 0;
 }
+// ... and, in kernels that walk BVHs under instances, the lane's save slots (the top-level
+// ray, the return link and -- the general kernel -- a hit's outer chain, while the lane walks
+// such a tree) in 7 or 8 more f64 fields at the end when the block's LDS has room for them
+// beside the whole mirror (KArgs::nest_lds): written at each tree entry, read at its THR_RET.
+// Else in global memory (KParams::nest_save, slot-major; also the pilot's counting kernel).
+// Off by default: the one scene it helps by traffic (final_scene: 9x fewer fabric writes) lost
+// 5% to the mirror records the slots displace, and the run-time choice between the two homes
+// cost final_scene 2% more in the kernel that has both (profiles/r06/ab_nest_save_lds.txt).
+#ifndef GS_NEST_SAVE_LDS
+#define GS_NEST_SAVE_LDS 0
+#endif
+__host__ __device__ constexpr uint32_t nest_save_lds(int feat) {
+    return (GS_NEST_SAVE_LDS && (feat & GS_FEAT_NESTED) != 0 && (feat & GS_FEAT_VISITS) == 0)
+               ? ((feat & GS_FEAT_GENERAL) ? 8u : 7u)
+               : 0u;
+}
 __host__ __device__ constexpr uint32_t lane_nd(bool chunked, int feat) {
     return (chunked ? (uint32_t)L_ND_CHUNKED : (uint32_t)L_ND) + (t_in_lds(feat) ? 3u : 0u);
 }
@@ -1332,8 +1410,8 @@ __host__ __device__ constexpr bool ninst_in_lds(int feat) {
 }
 __host__ __device__ constexpr uint32_t lane_ninst(int feat) { return (uint32_t)L_NI + (t_in_lds(feat) ? 1u : 0u); }
 __host__ __device__ constexpr uint32_t lane_ni(int feat) { return lane_ninst(feat) + (ninst_in_lds(feat) ? 1u : 0u); }
-__host__ __device__ constexpr size_t lane_lds_bytes(bool chunked, int feat) {
-    return (size_t)GS_BLOCK * (lane_nd(chunked, feat) * 8 + lane_ni(feat) * 4) + 128 + GS_STAMP_LDS;
+__host__ __device__ constexpr size_t lane_lds_bytes(bool chunked, int feat, uint32_t nsave = 0) {
+    return (size_t)GS_BLOCK * ((lane_nd(chunked, feat) + nsave) * 8 + lane_ni(feat) * 4) + 128 + GS_STAMP_LDS;
 }
 
 template <int FEAT>
@@ -1394,6 +1472,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     // A fixed-spp chunked launch (the host's choice, kernel_for): P->chunk != 0, no rounds, no
     // per-sample colours, max_depth > 0 -- a camera ray is always due when advance() runs.
     constexpr bool kFixed = (FEAT & GS_FEAT_FIXED) != 0;
+    constexpr bool kGeneral = (FEAT & GS_FEAT_GENERAL) != 0;
     // (t_in_lds kernels: the throughput's three fields first, at fixed offsets)
 #define LD(k) s_d[((k) + (t_in_lds(FEAT) ? 3 : 0)) * GS_BLOCK + tid]
 #define LI(k) s_i[(k) * GS_BLOCK + tid]
@@ -1403,6 +1482,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     uint32_t ninst_ = GS_REF_NONE;
 #define LNINST (*(ninst_in_lds(FEAT) ? &s_i[lane_ninst(FEAT) * GS_BLOCK + tid] : &ninst_))
     if constexpr (kNested) LNINST = GS_REF_NONE;
+    // the lane's nested-walk save slot k: the last f64 lane fields (nest_save_lds), else the
+    // slot-major global array (slot k of every lane of the grid contiguous)
+    double* const s_save = s_d + (size_t)(A.lane_nd - A.nest_lds) * GS_BLOCK + tid;
+    const size_t g_lanes = (size_t)gridDim.x * GS_BLOCK;
+#define NSAVE(k)                                                                                   \
+    (*(nest_save_lds(FEAT) && A.nest_lds ? &s_save[(size_t)(k) * GS_BLOCK]                         \
+                                         : &P->nest_save[(size_t)(k) * g_lanes + (size_t)blockIdx.x * GS_BLOCK + tid]))
 
     uint32_t st = S_NEED;
     bool qdone = false;
@@ -2016,10 +2102,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 GS_STAMP(rt0_);
 #endif
                 if (cur == THR_RET) {
-                    const double* sv = P->nest_save + ((size_t)blockIdx.x * GS_BLOCK + tid) * 8u;
-                    ray.o = mk(sv[0], sv[1], sv[2]);
-                    ray.d = mk(sv[3], sv[4], sv[5]);
-                    cur = (uint32_t)__double_as_longlong(sv[6]);
+                    ray.o = mk(NSAVE(0), NSAVE(1), NSAVE(2));
+                    ray.d = mk(NSAVE(3), NSAVE(4), NSAVE(5));
+                    cur = (uint32_t)__double_as_longlong(NSAVE(6));
                     LNINST = GS_REF_NONE;
                 }
                 GS_REGION(6, rt0_);  // (stamps: return passes)
@@ -2192,14 +2277,15 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         // (a primitive or list in the tree under LNINST; an instance leaf's own chain;
                         // round 6: an instance leaf inside the tree under LNINST -- both chains, the
                         // outer one in the save slot, bit 31 on the inner one)
-                        if constexpr (kNested) {
+                        if constexpr (kNested && kGeneral) {
                             if (lh.inst != GS_REF_NONE && LNINST != GS_REF_NONE) {
-                                P->nest_save[((size_t)blockIdx.x * GS_BLOCK + tid) * 8u + 7u] =
-                                    __longlong_as_double((long long)LNINST);
+                                NSAVE(7) = __longlong_as_double((long long)LNINST);
                                 LI(L_HINST) = lh.inst | 0x80000000u;
                             } else {
                                 LI(L_HINST) = lh.inst != GS_REF_NONE ? lh.inst : LNINST;
                             }
+                        } else if constexpr (kNested) {
+                            LI(L_HINST) = lh.inst != GS_REF_NONE ? lh.inst : LNINST;
                         } else {
                             LI(L_HINST) = lh.inst;
                         }
@@ -2210,14 +2296,13 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         // order, with its ray in the tree's space; the top-level ray and the
                         // link after this leaf wait in the lane's save slot until THR_RET.
                         if (lh.enter) {
-                            double* sv = P->nest_save + ((size_t)blockIdx.x * GS_BLOCK + tid) * 8u;
-                            sv[0] = ray.o.x;
-                            sv[1] = ray.o.y;
-                            sv[2] = ray.o.z;
-                            sv[3] = ray.d.x;
-                            sv[4] = ray.d.y;
-                            sv[5] = ray.d.z;
-                            sv[6] = __longlong_as_double((long long)next);
+                            NSAVE(0) = ray.o.x;
+                            NSAVE(1) = ray.o.y;
+                            NSAVE(2) = ray.o.z;
+                            NSAVE(3) = ray.d.x;
+                            NSAVE(4) = ray.d.y;
+                            NSAVE(5) = ray.d.z;
+                            NSAVE(6) = __longlong_as_double((long long)next);
                             LNINST = ref;
                             ray.o = rl.o;
                             ray.d = rl.d;
@@ -2317,7 +2402,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     uint64_t g2 = rng;
                     double c2 = closest;
                     asm volatile("" : "+v"(r2.d.x), "+v"(c2));
-                    const ShadeOut s2 = shade<(FEAT & GS_FEAT_PLAIN) != 0, kSphLeaf>(sc, r2, c2, hit_ref, LI(L_HINST), g2, s_cnt);
+                    const ShadeOut s2 = shade<(FEAT & GS_FEAT_PLAIN) != 0, kSphLeaf, kGeneral>(sc, r2, c2, hit_ref, LI(L_HINST), g2, s_cnt);
                     asm volatile("" ::"v"(s2.col.x), "v"(s2.col.y), "v"(s2.col.z), "v"(s2.dir.x), "v"(s2.dir.y), "v"(s2.dir.z),
                                  "v"(r2.o.x), "v"(g2), "v"(s2.cont));
                 }
@@ -2325,14 +2410,14 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 // (GS_FEAT_NESTED: a hit through a chain inside a BVH under another chain carries
                 // bit 31 on its inner chain's ref, the outer chain in the lane's save slot 7)
                 uint32_t hinst = (FEAT & GS_FEAT_PLAIN) ? GS_REF_NONE : LI(L_HINST), houter = GS_REF_NONE;
-                if constexpr (kNested) {
+                if constexpr (kNested && kGeneral) {
                     if (hinst != GS_REF_NONE && (hinst >> 31)) {
-                        houter = (uint32_t)__double_as_longlong(P->nest_save[((size_t)blockIdx.x * GS_BLOCK + tid) * 8u + 7u]);
+                        houter = (uint32_t)__double_as_longlong(NSAVE(7));
                         hinst &= 0x7FFFFFFFu;
                     }
                 }
-                const ShadeOut s = shade<(FEAT & GS_FEAT_PLAIN) != 0, kSphLeaf>(sc, ray, closest, hit_ref, hinst, rng, s_cnt,
-                                                                              houter);
+                const ShadeOut s = shade<(FEAT & GS_FEAT_PLAIN) != 0, kSphLeaf, kGeneral>(sc, ray, closest, hit_ref, hinst,
+                                                                                        rng, s_cnt, houter);
                 GS_MARK("shade_end");
                 GS_REGION(2, r0);
                 if (s.cont) {
@@ -2366,7 +2451,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     atomicAdd(&s_cnt[C_HITS], 1ull);
                     GS_STAMP(r0);
                     const HitRec h = kSphLeaf ? reconstruct_sphere<true>(sc, ray, closest, hit_ref)
-                                              : reconstruct(sc, ray, closest, hit_ref, LI(L_HINST));
+                                              : reconstruct<false>(sc, ray, closest, hit_ref, LI(L_HINST));
                     GS_REGION(1, r0);
                     GS_STAMP(r0);
                     const Scatter s = scatter(sc, h, ray.d, rng, s_cnt);
@@ -2444,6 +2529,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #undef LD
 #undef LI
 #undef LNINST
+#undef NSAVE
 #undef Tr
 #undef Tg
 #undef Tb
@@ -2811,7 +2897,7 @@ struct LaunchSlot {
     // batch rounds (adaptive settings): round counts, the two active lists, the running sums
     void* rbuf = nullptr;
     size_t rbuf_bytes = 0;
-    // GS_FEAT_NESTED: each lane's save slot (KParams::nest_save), 64 B per lane of the grid
+    // GS_FEAT_NESTED: each lane's save slots (KParams::nest_save), 8 slot-major arrays of 8 B per lane of the grid
     double* nest_save = nullptr;
     size_t nest_save_bytes = 0;
 };
@@ -2869,7 +2955,7 @@ struct gs_device_scene {
     // instantiation (feat minus GS_FEAT_LDSTREE when the mirror is a strict prefix), blocks/CU.
     struct LaunchCfg {
         bool ready = false;
-        uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_cubes = 0;
+        uint32_t lds_nodes = 0, lds_leaves = 0, lds_quads = 0, lds_cubes = 0, nest_lds = 0;
         size_t lds = 0;
         int feat = 0, per_cu = 0;
     } lcfg[2];
@@ -3080,7 +3166,10 @@ static Placed place_records(const ThreadedTree& t, const std::vector<uint64_t>* 
 // error code, never a GPU fault.
 // inst_reached (out): per instance, whether a leaf reachable from the root walks it (the scene
 // upload threads the BVHs under reached instances only).
-gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out, std::vector<uint8_t>* inst_reached) {
+gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out, std::vector<uint8_t>* inst_reached,
+                   bool* general_out, std::vector<uint8_t>* media_reached) {
+    media_reached->assign(s.n_media, 0);
+    bool general = false;  // a composition only GS_FEAT_GENERAL kernels walk (round 6)
     auto bad = [](const std::string& m) { return fail(GS_ERR_ARG, "invalid flat scene: " + m); };
     auto unsup = [](const std::string& m) { return fail(GS_ERR_UNSUPPORTED, m); };
     if (!s.nodes && s.n_nodes) return bad("nodes");
@@ -3108,6 +3197,7 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
             uint32_t i = cur & GS_REF_MASK;
             if (i >= s.n_instances) return 1;
             if (++chain > GS_MAX_CHAIN) return 2;
+            if (chain > 4) general = true;  // (the other kernels' hit record keeps 4)
             (*inst_reached)[i] = std::max((*inst_reached)[i], mark);
             const gs_instance& in = s.instances[i];
             if (in.kind != GS_INST_TRANSLATE && in.kind != GS_INST_ROTATE_Y) return 1;
@@ -3134,16 +3224,51 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
     // most GS_NESTED_STACK (the device walk is threaded and needs no stack; the bound keeps
     // the host's threading finite).  Subtrees may be shared between chains (instancing);
     // the depth bound ends cycles and a visit budget ends blow-ups.
-    // A ConstantMedium: its boundary a primitive or list behind an optional chain.
-    auto medium_ok = [&](uint32_t cur) -> int {
+    // A BVH as a medium boundary (GS_FEAT_GENERAL, tree_test): nodes in range, leaves lists or
+    // primitives, depth bounded (threaded with the BVHs under instances).
+    uint64_t boundary_budget = 64ull << 20;
+    auto boundary_tree_ok = [&](uint32_t root) -> int {
+        std::vector<std::pair<uint32_t, uint32_t>> st{{root, 1u}};
+        while (!st.empty()) {
+            auto [r, d] = st.back();
+            st.pop_back();
+            if (boundary_budget-- == 0) return 1;
+            if ((r >> GS_REF_SHIFT) == GS_REF_NODE) {
+                const uint32_t i = r & GS_REF_MASK;
+                if (i >= s.n_nodes) return 1;
+                if (d > GS_NESTED_STACK) return 2;
+                if (s.nodes[i].left == GS_REF_NONE) return 1;
+                st.push_back({s.nodes[i].left, d + 1});
+                if (s.nodes[i].right != GS_REF_NONE) st.push_back({s.nodes[i].right, d + 1});
+            } else {
+                const int e = shape_ok(r);
+                if (e) return e;
+            }
+        }
+        return 0;
+    };
+    // A ConstantMedium: its boundary a primitive or list behind an optional chain; round 6
+    // (GS_FEAT_GENERAL): also a BVH, or one level of another medium.
+    std::function<int(uint32_t, int)> medium_ok_l = [&](uint32_t cur, int level) -> int {
         uint32_t i = cur & GS_REF_MASK;
         if (i >= s.n_media || !s.media) return 1;
         if (s.media[i].material >= s.n_materials) return 1;
         uint32_t b = s.media[i].boundary;
         const int e = chain_ok(b, 2);
+        (*media_reached)[i] = 1;
         if (e) return e;
+        if ((b >> GS_REF_SHIFT) == GS_REF_NODE) {
+            general = true;
+            return boundary_tree_ok(b);
+        }
+        if ((b >> GS_REF_SHIFT) == GS_REF_MEDIUM) {
+            if (level > 0) return 2;  // media two deep inside media
+            general = true;
+            return medium_ok_l(b, level + 1);
+        }
         return shape_ok(b);
     };
+    auto medium_ok = [&](uint32_t cur) -> int { return medium_ok_l(cur, 0); };
     bool nested = false;
     uint64_t nested_budget = 64ull << 20;
     auto nested_ok = [&](uint32_t root) -> int {
@@ -3166,6 +3291,7 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
                 uint32_t c = r;
                 int e = chain_ok(c);
                 if (!e) {
+                    if (c != r) general = true;  // a chain inside the tree: two-chain hit records
                     if ((c >> GS_REF_SHIFT) == GS_REF_NODE) e = 2;
                     else e = (c >> GS_REF_SHIFT) == GS_REF_MEDIUM ? medium_ok(c) : shape_ok(c);
                 }
@@ -3212,6 +3338,7 @@ gs_status validate(const gs_flat_scene& s, uint32_t* depth_out, bool* nested_out
     }
     *depth_out = maxd;
     *nested_out = nested;
+    *general_out = general;
     auto mat_ok = [&](uint32_t m) { return m < s.n_materials; };
     for (uint32_t i = 0; i < s.n_spheres; i++) if (!mat_ok(s.spheres[i].material)) return bad("sphere material");
     for (uint32_t i = 0; i < s.n_mspheres; i++) if (!mat_ok(s.mspheres[i].material)) return bad("msphere material");
@@ -3363,9 +3490,9 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     if (!s || !out) return fail(GS_ERR_ARG, "null argument");
     *out = nullptr;
     uint32_t depth = 1;
-    bool nested = false;
-    std::vector<uint8_t> inst_reached;
-    gs_status v = validate(*s, &depth, &nested, &inst_reached);
+    bool nested = false, general = false;
+    std::vector<uint8_t> inst_reached, media_reached;
+    gs_status v = validate(*s, &depth, &nested, &inst_reached, &general, &media_reached);
     if (v != GS_OK) return v;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(GS_ERR_NO_DEVICE, "no HIP device visible");
@@ -3519,6 +3646,60 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
             std::unordered_map<uint32_t, uint32_t> tree_of;  // gs node index -> tree
             std::vector<double> tree_score;                   // a tree's best entry (its leaves' score)
             std::vector<uint32_t> tree_depth;
+            // thread the tree at BVH node ref `node_ref` once; returns its tree index
+            auto thread_tree = [&](uint32_t node_ref) -> uint32_t {
+                const uint32_t root = node_ref & GS_REF_MASK;
+                auto it = tree_of.find(root);
+                if (it != tree_of.end()) return it->second;
+                const uint32_t first = (uint32_t)thr.size();
+                struct Work {
+                    uint32_t x;
+                    bool close;
+                };
+                std::vector<Work> work{{node_ref, false}};
+                while (!work.empty()) {
+                    const Work w = work.back();
+                    work.pop_back();
+                    if (w.close) {
+                        thr[w.x].right = (uint32_t)thr.size();
+                        continue;
+                    }
+                    const uint32_t idx = (uint32_t)thr.size();
+                    DNode rec{};
+                    if ((w.x >> GS_REF_SHIFT) == GS_REF_NODE) {
+                        const gs_node& nd = s->nodes[w.x & GS_REF_MASK];
+                        rec = DNode{nd.min[0], nd.min[1], nd.min[2], nd.max[0], nd.max[1], nd.max[2], idx + 1u, 0u, 0u, 0u};
+                        thr.push_back(rec);
+                        thr_leaf.push_back(0);
+                        work.push_back({idx, true});
+                        if (nd.right != GS_REF_NONE) work.push_back({nd.right, false});
+                        work.push_back({nd.left, false});
+                    } else {
+                        if ((w.x >> GS_REF_SHIFT) == GS_REF_SPHERE) {
+                            const gs_sphere& q = s->spheres[w.x & GS_REF_MASK];
+                            rec.mnx = q.center[0];
+                            rec.mny = q.center[1];
+                            rec.mnz = q.center[2];
+                            rec.mxx = q.radius;
+                        }
+                        rec.left = idx + 1u;
+                        rec.right = w.x;
+                        thr.push_back(rec);
+                        thr_leaf.push_back(1);
+                    }
+                }
+                const uint32_t end = (uint32_t)thr.size();
+                for (uint32_t k = first; k < end; k++) {
+                    if (thr[k].left == end) thr[k].left = RAW_RET;
+                    if (!thr_leaf[k] && thr[k].right == end) thr[k].right = RAW_RET;
+                }
+                const uint32_t tr = (uint32_t)nroot_rec_keep.size();
+                tree_of.emplace(root, tr);
+                nroot_rec_keep.push_back(first);
+                tree_score.push_back(0.0);
+                tree_depth.push_back(0);
+                return tr;
+            };
             for (size_t ii = 0; ii < insts.size(); ii++) {
                 gs_instance& in = insts[ii];
                 if ((in.child >> GS_REF_SHIFT) != GS_REF_NODE) continue;
@@ -3529,58 +3710,14 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                     in.child = GS_REF_NONE;
                     continue;
                 }
-                const uint32_t root = in.child & GS_REF_MASK;
-                auto it = tree_of.find(root);
-                if (it == tree_of.end()) {
-                    const uint32_t first = (uint32_t)thr.size();
-                    struct Work {
-                        uint32_t x;
-                        bool close;
-                    };
-                    std::vector<Work> work{{in.child, false}};
-                    while (!work.empty()) {
-                        const Work w = work.back();
-                        work.pop_back();
-                        if (w.close) {
-                            thr[w.x].right = (uint32_t)thr.size();
-                            continue;
-                        }
-                        const uint32_t idx = (uint32_t)thr.size();
-                        DNode rec{};
-                        if ((w.x >> GS_REF_SHIFT) == GS_REF_NODE) {
-                            const gs_node& nd = s->nodes[w.x & GS_REF_MASK];
-                            rec = DNode{nd.min[0], nd.min[1], nd.min[2], nd.max[0], nd.max[1], nd.max[2], idx + 1u, 0u, 0u, 0u};
-                            thr.push_back(rec);
-                            thr_leaf.push_back(0);
-                            work.push_back({idx, true});
-                            if (nd.right != GS_REF_NONE) work.push_back({nd.right, false});
-                            work.push_back({nd.left, false});
-                        } else {
-                            if ((w.x >> GS_REF_SHIFT) == GS_REF_SPHERE) {
-                                const gs_sphere& q = s->spheres[w.x & GS_REF_MASK];
-                                rec.mnx = q.center[0];
-                                rec.mny = q.center[1];
-                                rec.mnz = q.center[2];
-                                rec.mxx = q.radius;
-                            }
-                            rec.left = idx + 1u;
-                            rec.right = w.x;
-                            thr.push_back(rec);
-                            thr_leaf.push_back(1);
-                        }
-                    }
-                    const uint32_t end = (uint32_t)thr.size();
-                    for (uint32_t k = first; k < end; k++) {
-                        if (thr[k].left == end) thr[k].left = RAW_RET;
-                        if (!thr_leaf[k] && thr[k].right == end) thr[k].right = RAW_RET;
-                    }
-                    it = tree_of.emplace(root, (uint32_t)nroot_rec_keep.size()).first;
-                    nroot_rec_keep.push_back(first);
-                    tree_score.push_back(0.0);
-                    tree_depth.push_back(0);
-                }
-                in.child = GS_MAKE_REF(GS_REF_NODE, it->second);
+                in.child = GS_MAKE_REF(GS_REF_NODE, thread_tree(in.child));
             }
+            // (GS_FEAT_GENERAL) a BVH that is a medium's boundary with no chain: threaded alike,
+            // the medium's device boundary the tree's ref (tree_test)
+            if (general)
+                for (size_t mi = 0; mi < media.size(); mi++)
+                    if (media_reached[mi] && (media[mi].boundary >> GS_REF_SHIFT) == GS_REF_NODE)
+                        media[mi].boundary = GS_MAKE_REF(GS_REF_NODE, thread_tree(media[mi].boundary));
             if (nroot_rec_keep.size() > GS_REF_MASK) return fail(GS_ERR_UNSUPPORTED, "too many BVHs under instances");
             // Static estimate for the nested records: a top-level leaf whose chain ends in a
             // tree gives it its score and depth; inside, the smallest surface area on the path
@@ -3784,6 +3921,9 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
     d.hdri_rgbe = rgbe.empty() ? nullptr : (const uint32_t*)(b + o_rgbe);
     d.bg = s->background;
     d.root = device_ref(s->root);
+    d.tnodes = (const TNode*)(b + o_tnodes);
+    d.tboxes = (const TBox*)(b + o_tboxes);
+    d.tleaves = (const TLeaf*)(b + o_tleaves);
     for (int k = 0; k < kLaunchSlots; k++) {
         ds->slots[k].queue = (uint32_t*)(b + o_slot[k]);
         ds->slots[k].params = (KParams*)(b + o_slot[k] + 256);
@@ -3835,6 +3975,8 @@ gs_status gs_device_scene_create(const gs_flat_scene* s, gs_device_scene** out) 
                       m.kind == DM_DIELECTRIC) && !m.needs_uv;
         if (plain) ds->feat |= GS_FEAT_PLAIN;
     }
+    // compositions only the catch-all instantiation walks (round 6; validate)
+    if (general) ds->feat = GS_FEAT_GENERAL_KERNEL;
     ds->cert_boxes = cert_boxes;
     ds->node_steps = auto_node_steps;
     // Scenes with BVHs under instances (kind-batched leaf passes over many leaf kinds) gather
@@ -3966,6 +4108,7 @@ static void (*kernel_for(int feat))(KArgs) {
         GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_LDSTREE)
         GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_PLAIN)
         GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_PLAIN | GS_FEAT_LDSTREE)
+        GS_K(GS_FEAT_GENERAL_KERNEL)
         GS_K(GS_FEAT_SPHLEAF)
         GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LDSTREE)
         GS_K(GS_FEAT_SPHLEAF | GS_FEAT_MIXED)
@@ -4214,13 +4357,18 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         HIPCHK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
         // The node mirror must start at LDS address 0 (load_tnode): no static LDS.
         if (fa.sharedSizeBytes != 0) return fail(GS_ERR_UNSUPPORTED, "render kernel with static LDS");
-        const int64_t room = (int64_t)max_lds - (int64_t)lane_lds_bytes(chunked, ds->feat);
-        if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
         uint32_t ln = ds->lds_nodes, ll = ds->lds_leaves, lq = ds->lds_quads, lk = ds->lds_cubes;
         auto bytes = [&] {
             return (int64_t)ln * (int64_t)sizeof(TNode) + (int64_t)ll * (int64_t)sizeof(TLeaf) +
                    (int64_t)lq * (int64_t)sizeof(TQuad) + (int64_t)lk * (GS_CUBE_DOUBLES * 8);
         };
+        // (the nested walk's save slots too, when they displace no mirror record; else they
+        // stay in global memory: final_scene, whose mirror wants more than the 24 KiB the
+        // slots would leave, lost 5% with them in LDS -- profiles/r06/ab_nest_save_lds.txt)
+        uint32_t nsave = nest_save_lds(ds->feat);
+        if ((int64_t)max_lds - (int64_t)lane_lds_bytes(chunked, ds->feat, nsave) < bytes()) nsave = 0;
+        const int64_t room = (int64_t)max_lds - (int64_t)lane_lds_bytes(chunked, ds->feat, nsave);
+        if (room < 0) return fail(GS_ERR_UNSUPPORTED, "lane state exceeds the device's LDS per block");
         // shrink the least valuable prefix first: cubes, quads, then all
         while (bytes() > room && lk) lk = lk - 1 - lk / 16;
         while (bytes() > room && lq) lq = lq - 1 - lq / 16;
@@ -4232,7 +4380,8 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         lc.lds_leaves = ll;
         lc.lds_quads = lq;
         lc.lds_cubes = lk;
-        lc.lds = lane_lds_bytes(chunked, ds->feat) + (size_t)bytes();
+        lc.lds = lane_lds_bytes(chunked, ds->feat, nsave) + (size_t)bytes();
+        lc.nest_lds = nsave;
         lc.feat = ds->feat;
         if (ln < ds->node_records || ll < ds->leaf_records) lc.feat &= ~GS_FEAT_LDSTREE;
         int occ = 0;
@@ -4247,7 +4396,8 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     a.lds_quads = lc.lds_quads;
     a.lds_cubes = lc.lds_cubes;
     a.cubes = ds->dev.cubes;
-    a.lane_nd = lane_nd(chunked, ds->feat);
+    a.lane_nd = lane_nd(chunked, ds->feat) + lc.nest_lds;
+    a.nest_lds = lc.nest_lds;
     const int32_t t_bpc = g_blocks_per_cu.load(std::memory_order_relaxed);
     const int per_cu = t_bpc > 0 ? t_bpc : lc.per_cu;
     int64_t blocks = (int64_t)cus * per_cu;
@@ -4513,7 +4663,10 @@ static gs_status pilot_end(gs_device_scene* ds, PilotRun& pr) {
 static bool pilot_due(gs_device_scene* ds, const gs_camera* cam, const gs_sample_settings* ss) {
     if (ds->placement.load(std::memory_order_acquire) != 0) return false;
     const bool all_mirrored = ds->lds_nodes == ds->node_records && ds->lds_leaves == ds->leaf_records;
-    if (!g_placement || all_mirrored || !cam || cam->image_width <= 0 || cam->image_height <= 0) {
+    // (scenes of the catch-all kernel keep the static placement: the pilot's instantiation does
+    // not walk their compositions)
+    if (!g_placement || all_mirrored || !cam || cam->image_width <= 0 || cam->image_height <= 0 ||
+        (ds->feat & GS_FEAT_GENERAL)) {
         ds->placement.store(1, std::memory_order_release);
         return false;
     }

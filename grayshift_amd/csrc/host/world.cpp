@@ -378,14 +378,15 @@ uint32_t RotateY::flatten(Flattener& f) const {
     return GS_MAKE_REF(GS_REF_INSTANCE, idx);
 }
 uint32_t BVHNode::flatten(Flattener& f) const {
-    if (f.inside_medium) throw std::domain_error("BVH as a ConstantMedium boundary is not supported on the device path");
+    // (round 6: a BVH as a ConstantMedium boundary is walked by the device's catch-all kernel;
+    // its leaves must be lists or primitives -- the device's validation says so otherwise)
     if (f.instance_in_nested)
         throw std::domain_error("a BVH under Translate/RotateY inside a BVH that is itself under Translate/RotateY "
                                 "(two levels of nested BVHs) is not supported on the device path");
     // A BVH under Translate/RotateY (final_scene's balls, main.rs:741-755) is walked by the
     // device as a second-level tree on its own stack: its depth does not count towards
     // the top-level (LDS) stack.
-    const bool top = !f.inside_instance;
+    const bool top = !f.inside_instance && f.medium_depth == 0;
     const bool was_nested = f.inside_nested_bvh;
     if (!top) f.inside_nested_bvh = true;
     // Pre-order: the left subtree follows its parent in memory (cache locality).
@@ -409,16 +410,21 @@ uint32_t BVHNode::flatten(Flattener& f) const {
 }
 
 uint32_t ConstantMedium::flatten(Flattener& f) const {  // volume.rs:10-29
-    if (f.inside_medium)
-        throw std::domain_error("ConstantMedium inside a ConstantMedium boundary is not supported on the device path");
+    // (round 6: one medium as another's boundary is walked by the device's catch-all kernel)
+    if (f.medium_depth >= 2)
+        throw std::domain_error("ConstantMedium two deep inside ConstantMedium boundaries is not supported on the "
+                                "device path");
     // (inside a BVH under Translate/RotateY: supported since round 5, the device walks such
     // trees in its main passes and tests their media like the top level's)
     size_t idx = f.media.size();
     check_index(idx, "media");
     f.media.push_back(gs_medium{});
+    const bool was = f.inside_medium;
     f.inside_medium = true;
+    f.medium_depth++;
     uint32_t b = boundary->flatten(f);
-    f.inside_medium = false;
+    f.medium_depth--;
+    f.inside_medium = was;
     uint32_t m = f.material_index(phase_function.get());
     gs_medium& md = f.media[idx];
     md.boundary = b;

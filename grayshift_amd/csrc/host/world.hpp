@@ -277,9 +277,9 @@ public:
     AABB bbox;
 };
 
-// hittable/volume.rs:10-68.  The boundary is any Hittable but a BVH or another medium
-// on the device path (flatten throws std::domain_error otherwise); the medium itself may sit
-// in a BVH under Translate/RotateY (round 5).
+// hittable/volume.rs:10-68.  The boundary is a primitive, a list, a BVH of those, or (one
+// level) another medium on the device path (round 6; the device's validation and flatten say
+// so otherwise); the medium itself may sit in a BVH under Translate/RotateY (round 5).
 class ConstantMedium : public Hittable {
 public:
     ConstantMedium(HittablePtr boundary, double density, MaterialPtr phase_function)
@@ -342,6 +342,7 @@ public:
     uint32_t depth = 0, max_depth = 0;  // BVH node nesting while flattening
     bool inside_instance = false;
     bool inside_medium = false;  // flattening a ConstantMedium boundary
+    int medium_depth = 0;        // ConstantMedium boundaries being flattened (round 6: up to 2)
     bool inside_nested_bvh = false;  // flattening a BVH under Translate/RotateY
     bool instance_in_nested = false;  // flattening a Translate/RotateY inside such a BVH (round 6)
 };

@@ -135,7 +135,8 @@ def test_adaptive_edge_settings(batch, maxs, tol):
 def test_unsupported_scene_fails_cleanly():
     b = g.SceneBuilder()
     m = b.lambertian((1, 1, 1))
-    b.add(b.medium(b.medium(b.sphere((0, 0, 0), 1, m), 0.5, m), 0.5, m))  # a medium as a medium's boundary
+    # media three deep (one medium as another's boundary is supported since round 6)
+    b.add(b.medium(b.medium(b.medium(b.sphere((0, 0, 0), 1, m), 0.5, m), 0.5, m), 0.5, m))
     sc = scenes.Scene("vol", b.build(), camera_spec(1.0, 8, 5, 40, (0, 0, 5), (0, 0, 0), (0, 1, 0), 0, 5),
                       fixed_spp(1))
     with pytest.raises(N.GrayshiftError) as e:
