@@ -12,7 +12,10 @@ instantiation (default FEAT=20: the C4 kernel, leaf runs + staged shading) and c
   ray (both listed on their own);
 * leaf pass: leaf_begin .. leaf_end minus the other-kind leaves (moving spheres, quads,
   triangles, lists, instances, media: listed on their own), i.e. the stationary-sphere
-  path with its leaf run (a run's second sphere counted statically once).
+  path with its leaf run (a run's second sphere counted statically once);
+* shade pass: shade_begin .. shade_end (hit record, scatter, throughput);
+* advance + get_ray: adv_begin .. adv_end (a finished sample's sums, the next item's claim,
+  the camera ray).
 
     python tools/isa_census.py [--feat 4] [--dump profiles/r02/isa_node_leaf.s]
 """
@@ -108,6 +111,11 @@ def main():
                "  f64 test blocks (rare paths)": node64,
                "leaf pass (head, links, run)": k[lb:sph_b] + k[sph_e:ob] + k[oe:le],
                "  stationary-sphere test": k[sph_b:sph_e], "  other leaf kinds": k[ob:oe]}
+    # the shade pass (hit record, material scatter, throughput) and the sample advance
+    # (chunk sums, refill, camera ray: get_ray) when the instantiation has their marks
+    for nm, b, e in (("shade pass", "shade_begin", "shade_end"), ("advance + get_ray", "adv_begin", "adv_end")):
+        if b in marks and e in marks:
+            regions[nm] = k[marks[b][0]:marks[e][-1]]
     print("gs_render_kernel<%d> (gfx950, static instruction counts)" % a.feat)
     print("%-32s %6s %6s %6s %6s %6s %6s" % ("region", "VALU", "(f64)", "SALU", "VMEM", "LDS", "ctrl"))
     for n, r in regions.items():
