@@ -69,6 +69,14 @@ using namespace gsd;
 #ifndef GS_ROUND_WHOLE_MAX_BATCH
 #define GS_ROUND_WHOLE_MAX_BATCH 256
 #endif
+// A split round's per-sample colours: entry a's sample j at j * n + a (sample-major: the
+// combine's lanes read one contiguous run per sample), or at a * batch + j (pixel-major: a
+// wave's 1-sample items write one contiguous run).  MI355X A2 (round 6): equal render time;
+// fabric writes 20.1 vs 15.0 GB a frame, combine 4.2 vs 5.7 ms a frame (5.7 -> 6.2 ms with the
+// pixels' samples staged through LDS); profiles/r06/ab_A2_round_items.txt
+#ifndef GS_ROUND_PIXEL_MAJOR
+#define GS_ROUND_PIXEL_MAJOR 0
+#endif
 #define GS_NESTED_STACK 32  // max depth of a BVH under a Translate/RotateY chain (a validation bound; the walk is stackless)
 // Kernel feature flags (template argument): scenes without them compile the code out.
 #define GS_FEAT_MEDIA 1   // ConstantMedium leaves (RNG draws inside traversal)
@@ -97,6 +105,10 @@ using namespace gsd;
 #define GS_FEAT_FIXED 128  // a fixed-spp launch in sample chunks (KParams.chunk != 0, no batch rounds,
                            // max_depth > 0): the adaptive loop's batch ends, stop test, Σlum / Σlum²
                            // and the rounds' per-sample colours are compiled out (round 6)
+#define GS_FEAT_RSPLIT 1024  // with GS_FEAT_FIXED: a batch round of split items (KParams.per_sample,
+                             // chunk != 0, max_depth > 0) -- the fixed kernel's sample loop, its items
+                             // taken from the round's active list and each sample's colour written for
+                             // the combine; no stop test, Σlum or batch end in the kernel (round 6)
 #ifndef GS_NODE_STEPS
 #define GS_NODE_STEPS 8  // node steps per unrolled node pass (the render kernel, below)
 #endif
@@ -249,6 +261,7 @@ struct KParams {
     uint32_t* next_active;     // the next round's, appended by the combine
     uint32_t* active_buf[2];   // the two lists (rounds alternate)
     uint32_t* round_counts;    // [rounds + 1]: active pixels per round
+    unsigned long long* rpp_hint;  // [2]: rays, paths of the slot's last split rounds (item sizes; kept across launches)
     double* pstate;            // per packed pixel: the running Σr, Σg, Σb, Σlum, Σlum² (camera.rs:131-146)
     // GS_FEAT_NESTED: per lane (block * GS_BLOCK + thread), the top-level ray while the lane
     // walks a BVH under an instance chain: o, d (6 doubles), the return link (u32), and (the
@@ -1422,7 +1435,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     extern __shared__ __align__(16) uint8_t smem[];
     // An empty batch round (adaptive settings: no active pixel left in this segment) has no
     // item to hand out: return before the mirror copy.
-    if (!(FEAT & GS_FEAT_FIXED) && A.P->rounds && A.P->n_items == 0) return;
+    if ((!(FEAT & GS_FEAT_FIXED) || (FEAT & GS_FEAT_RSPLIT)) && A.P->rounds && A.P->n_items == 0) return;
 
     // The records a ray most likely tests (placed first by the host) are mirrored in LDS;
     // a lane whose node / leaf index is below lds_nodes / lds_leaves reads it from there
@@ -1472,6 +1485,8 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     // A fixed-spp chunked launch (the host's choice, kernel_for): P->chunk != 0, no rounds, no
     // per-sample colours, max_depth > 0 -- a camera ray is always due when advance() runs.
     constexpr bool kFixed = (FEAT & GS_FEAT_FIXED) != 0;
+    // ... or a batch round's split items in that form (GS_FEAT_RSPLIT: per-sample colours)
+    constexpr bool kRsplit = kFixed && (FEAT & GS_FEAT_RSPLIT) != 0;
     constexpr bool kGeneral = (FEAT & GS_FEAT_GENERAL) != 0;
     // (t_in_lds kernels: the throughput's three fields first, at fixed offsets)
 #define LD(k) s_d[((k) + (t_in_lds(FEAT) ? 3 : 0)) * GS_BLOCK + tid]
@@ -1538,10 +1553,10 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 
     // camera.rs:142-146 for one finished sample of colour L
     auto add_sample = [&](double Lr, double Lg, double Lb) {
-        if (!kFixed && P->per_sample) {  // batch rounds: the sample's colour, summed in order by the combine
+        if (kRsplit || (!kFixed && P->per_sample)) {  // batch rounds: the sample's colour, summed in order by the combine
             double* o = P->partial + (size_t)LI(L_ITEM) * 3;
             st_partial(o, Lr, Lg, Lb);
-            LI(L_ITEM) += P->seg_n;
+            LI(L_ITEM) += GS_ROUND_PIXEL_MAJOR ? 1u : P->seg_n;
         } else {
             LD(L_CSR) += Lr;
             LD(L_CSG) += Lg;
@@ -1577,7 +1592,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
     };
     auto end_chunk = [&]() {
         const uint32_t item = LI(L_ITEM);
-        if (kFixed || !P->per_sample) {
+        if (!kRsplit && (kFixed || !P->per_sample)) {
             double* o = P->partial + (size_t)item * 3;
             st_partial(o, LD(L_CSR), LD(L_CSG), LD(L_CSB));
         }
@@ -1811,7 +1826,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     const uint32_t qr = fine ? q32 - P->fine_base : q32;
                     const uint32_t pr = udiv(qr, fine ? P->u_fcpp : P->u_cpp), ck = qr - pr * cpp;
                     uint32_t slot, x, y;
-                    if (!kFixed && P->rounds) {  // batch rounds: the packed pixel of active entry pr
+                    if (kRsplit || (!kFixed && P->rounds)) {  // batch rounds: the packed pixel of active entry pr
                         const uint32_t it = P->active[P->seg_base + pr];
                         slot = udiv(it, P->u_tpx);
                         const uint32_t w = it - slot * tile_px;
@@ -1857,9 +1872,9 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                         LD(L_CSR) = 0.0;
                         LD(L_CSG) = 0.0;
                         LD(L_CSB) = 0.0;
-                        if (!kFixed && P->per_sample) {
+                        if (kRsplit || (!kFixed && P->per_sample)) {
                             // batch rounds: the sample slots of entry pr, samples ck * csz on
-                            LI(L_ITEM) = ck * csz * P->seg_n + pr;
+                            LI(L_ITEM) = GS_ROUND_PIXEL_MAJOR ? pr * P->ss.batch_size + ck * csz : ck * csz * P->seg_n + pr;
                             LI(L_SAMPLE) = P->round_base + ck * csz;
                             LI(L_BLEFT) = min(csz, P->ss.batch_size - ck * csz);
                         } else if (kFixed || P->chunk) {
@@ -2703,10 +2718,31 @@ __global__ void gs_round_params_kernel(KParams* __restrict__ P, uint32_t round, 
     if (chunk_req > 0) {
         csz = min((uint32_t)chunk_req, bs);
     } else {
-        // (round 5: items of at least 2 or 4 samples, or 2 items per lane: +0.5%, -2.0%,
-        // -20% on A2, profiles/r05/ab_A2_round_item_sizes.txt)
-        csz = min(16u, bs);
-        while (csz > 1u && (uint64_t)n_seg * ((bs + csz - 1u) / csz) < 8ull * P->lanes) csz >>= 1;
+        // Scenes whose paths are long (>= 2 rays a path so far: the launch's counters from round
+        // 1 on, before that the slot's last rounds) take 1-sample items: a round then ends on one
+        // path, not on an item of several.  Round 6, MI355X A2 (cornell_box, 5.3 rays a path):
+        // the rule below for every scene 9 553 Msamples/s; 16 / 32 / 64 / 128 items per lane
+        // 10 216 / 10 767 / 10 955 / 10 954, the last two 1-sample items at A2's size.  Short
+        // paths (A1's hdri, 1.1) keep the rule -- halve 16-sample items until the round has 8
+        // items per lane: with 1-sample items A1 in rounds ran 10 968 instead of 23 729, each
+        // item's fixed costs beside a one-ray path (profiles/r06/ab_A2_round_items.txt).
+        // Item sizes are scheduling only: the combine folds every sample in order.
+        unsigned long long rays = 0, paths = 0;
+        if (round && P->counters) {
+            rays = P->counters[C_RAYS];
+            paths = P->counters[C_PATHS];
+            P->rpp_hint[0] = rays;
+            P->rpp_hint[1] = paths;
+        } else if (!round) {
+            rays = P->rpp_hint[0];
+            paths = P->rpp_hint[1];
+        }
+        if (paths && rays >= 2ull * paths) {
+            csz = 1u;
+        } else {
+            csz = min(16u, bs);
+            while (csz > 1u && (uint64_t)n_seg * ((bs + csz - 1u) / csz) < 8ull * P->lanes) csz >>= 1;
+        }
     }
     const uint32_t cpp = whole ? 1u : (bs + csz - 1u) / csz;
     P->per_sample = whole ? 0u : 1u;
@@ -2755,8 +2791,8 @@ __global__ void gs_round_combine_kernel(const KParams* __restrict__ P, uint32_t 
                 lsum = ps[3];
                 lsq = ps[4];
             }
-            const double* smp = P->partial + (size_t)a * 3;
-            for (uint32_t j = 0; j < bs; j++, smp += (size_t)n * 3) {
+            const double* smp = P->partial + (size_t)a * (GS_ROUND_PIXEL_MAJOR ? bs : 1u) * 3;
+            for (uint32_t j = 0; j < bs; j++, smp += (GS_ROUND_PIXEL_MAJOR ? 1u : (size_t)n) * 3) {
                 const double cr = smp[0], cg = smp[1], cb = smp[2];
                 r += cr;
                 g += cg;
@@ -4084,42 +4120,58 @@ static void (*kernel_for(int feat))(KArgs) {
     (void)feat;
     return gs_render_kernel<GS_ONLY_FEAT>;
 #else
-    // The product instantiations, each also in its fixed-spp form (| GS_FEAT_FIXED).
+    // The product instantiations, each also in its fixed-spp form (| GS_FEAT_FIXED); those
+    // without media or BVHs under instances also in the split batch-round form (| GS_FEAT_FIXED
+    // | GS_FEAT_RSPLIT; has_rsplit).
 #define GS_K(F)                                              \
     case (F): return gs_render_kernel<(F)>;                  \
     case (F) | GS_FEAT_FIXED: return gs_render_kernel<(F) | GS_FEAT_FIXED>;
+#define GS_KR(F) \
+    GS_K(F)      \
+    case (F) | GS_FEAT_FIXED | GS_FEAT_RSPLIT: return gs_render_kernel<(F) | GS_FEAT_FIXED | GS_FEAT_RSPLIT>;
     switch (feat) {
         GS_K(GS_FEAT_MEDIA)
         GS_K(GS_FEAT_NESTED)
         GS_K(GS_FEAT_MEDIA | GS_FEAT_NESTED)
-        GS_K(GS_FEAT_LEAFRUN)
+        GS_KR(GS_FEAT_LEAFRUN)
         GS_K(GS_FEAT_LEAFRUN | GS_FEAT_MEDIA)
         GS_K(GS_FEAT_LEAFRUN | GS_FEAT_NESTED)
         GS_K(GS_FEAT_LEAFRUN | GS_FEAT_MEDIA | GS_FEAT_NESTED)
-        GS_K(GS_FEAT_LDSTREE)
-        GS_K(GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN)
-        GS_K(GS_FEAT_MIXED)
-        GS_K(GS_FEAT_MIXED | GS_FEAT_LEAFRUN)
-        GS_K(GS_FEAT_MIXED | GS_FEAT_LDSTREE)
-        GS_K(GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN)
-        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN)
-        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_LDSTREE)
-        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED)
-        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_LDSTREE)
-        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_PLAIN)
-        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_PLAIN | GS_FEAT_LDSTREE)
+        GS_KR(GS_FEAT_LDSTREE)
+        GS_KR(GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN)
+        GS_KR(GS_FEAT_MIXED)
+        GS_KR(GS_FEAT_MIXED | GS_FEAT_LEAFRUN)
+        GS_KR(GS_FEAT_MIXED | GS_FEAT_LDSTREE)
+        GS_KR(GS_FEAT_MIXED | GS_FEAT_LDSTREE | GS_FEAT_LEAFRUN)
+        GS_KR(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN)
+        GS_KR(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_LDSTREE)
+        GS_KR(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED)
+        GS_KR(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_LDSTREE)
+        GS_KR(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_PLAIN)
+        GS_KR(GS_FEAT_SPHLEAF | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_PLAIN | GS_FEAT_LDSTREE)
         GS_K(GS_FEAT_GENERAL_KERNEL)
-        GS_K(GS_FEAT_SPHLEAF)
-        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_LDSTREE)
-        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_MIXED)
-        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_MIXED | GS_FEAT_LDSTREE)
-        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_MIXED | GS_FEAT_PLAIN)
-        GS_K(GS_FEAT_SPHLEAF | GS_FEAT_MIXED | GS_FEAT_PLAIN | GS_FEAT_LDSTREE)
+        GS_KR(GS_FEAT_SPHLEAF)
+        GS_KR(GS_FEAT_SPHLEAF | GS_FEAT_LDSTREE)
+        GS_KR(GS_FEAT_SPHLEAF | GS_FEAT_MIXED)
+        GS_KR(GS_FEAT_SPHLEAF | GS_FEAT_MIXED | GS_FEAT_LDSTREE)
+        GS_KR(GS_FEAT_SPHLEAF | GS_FEAT_MIXED | GS_FEAT_PLAIN)
+        GS_KR(GS_FEAT_SPHLEAF | GS_FEAT_MIXED | GS_FEAT_PLAIN | GS_FEAT_LDSTREE)
         case GS_FEAT_FIXED: return gs_render_kernel<GS_FEAT_FIXED>;
+        case GS_FEAT_FIXED | GS_FEAT_RSPLIT: return gs_render_kernel<GS_FEAT_FIXED | GS_FEAT_RSPLIT>;
         case GS_FEAT_PILOT: return gs_render_kernel<GS_FEAT_PILOT>;
         default: return gs_render_kernel<0>;
     }
+#undef GS_KR
 #undef GS_K
+#endif
+}
+// A split batch round may take the (F | FIXED | RSPLIT) instantiation (kernel_for's GS_KR list).
+static bool has_rsplit(int feat) {
+#ifdef GS_ONLY_FEAT
+    (void)feat;
+    return false;
+#else
+    return (feat & (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_GENERAL | GS_FEAT_VISITS)) == 0;
 #endif
 }
 
@@ -4460,8 +4512,9 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         }
         kp.partial = sl.partial;
     }
-    // batch rounds: [round counts][active list 0][active list 1][running sums], 256-B aligned
-    const size_t r_counts = ((size_t)(n_rounds + 2) * 4 + 255) & ~(size_t)255;
+    // batch rounds: [item-size hint, round counts][active list 0][active list 1][running sums],
+    // 256-B aligned (the hint first: it outlives launches of other settings)
+    const size_t r_counts = ((size_t)(n_rounds + 2) * 4 + 16 + 255) & ~(size_t)255;
     const size_t r_list = ((size_t)cap * 4 + 255) & ~(size_t)255;
     if (n_rounds) {
         const size_t need = r_counts + 2 * r_list + (size_t)cap * 5 * sizeof(double);
@@ -4473,9 +4526,11 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
             if (hipMalloc(&sl.rbuf, need) != hipSuccess)
                 return fail(GS_ERR_OOM, "hipMalloc of " + std::to_string(need) + " bytes of batch-round state failed");
             sl.rbuf_bytes = need;
+            HIPCHK(hipMemsetAsync(sl.rbuf, 0, 16, st));  // no item-size hint yet
         }
         uint8_t* rb = (uint8_t*)sl.rbuf;
-        kp.round_counts = (uint32_t*)rb;
+        kp.rpp_hint = (unsigned long long*)rb;
+        kp.round_counts = (uint32_t*)(rb + 16);
         kp.active_buf[0] = (uint32_t*)(rb + r_counts);
         kp.active_buf[1] = (uint32_t*)(rb + r_counts + r_list);
         kp.pstate = (double*)(rb + r_counts + 2 * r_list);
@@ -4498,6 +4553,9 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
     if (outs->item_visits) HIPCHK(hipMemsetAsync(outs->item_visits, 0, (size_t)cap * sizeof(uint32_t), st));
     hipLaunchKernelGGL(gs_params_kernel, dim3(1), dim3(64), 0, st, kp, sl.params);  // (zeroes the queue)
     HIPCHK(hipGetLastError());
+#ifndef GS_USE_RSPLIT
+#define GS_USE_RSPLIT 1  // (A/B: 0 runs split rounds on the generic instantiation)
+#endif
     if (n_rounds) {
         // init (every real packed pixel active), then per round and segment: parameters,
         // the megakernel, the combine; all on the stream, no host synchronisation (a segment
@@ -4509,11 +4567,18 @@ static gs_status launch(const gs_device_scene* ds, const gs_camera* cam, const g
         HIPCHK(hipGetLastError());
         if (k_begin) HIPCHK(hipEventRecord(k_begin, st));
         const unsigned g_comb = (unsigned)std::min<int64_t>((seg_px + 255) / 256, 8192);
+        // Rounds whose items are surely split (gs_round_params_kernel: a requested chunk, a batch
+        // above GS_ROUND_WHOLE_MAX_BATCH, or whole-batch items off -- the default) and whose
+        // paths always trace a camera ray take the fixed kernel's sample loop (GS_FEAT_RSPLIT).
+        const int32_t t_whole = g_round_whole.load(std::memory_order_relaxed);
+        const bool rsplit = GS_USE_RSPLIT && has_rsplit(lc.feat) && cam->max_depth > 0 &&
+                            (t_sample_chunk > 0 || ss->batch_size > GS_ROUND_WHOLE_MAX_BATCH || t_whole == 0);
+        void (*rkern)(KArgs) = kernel_for(rsplit ? lc.feat | GS_FEAT_FIXED | GS_FEAT_RSPLIT : lc.feat);
         for (uint32_t r = 0; r < n_rounds; r++)
             for (uint32_t sg = 0; sg < n_segs; sg++) {
                 hipLaunchKernelGGL(gs_round_params_kernel, dim3(1), dim3(64), 0, st, dP, r, sg, seg_px, t_sample_chunk,
-                                   g_round_whole.load(std::memory_order_relaxed));
-                hipLaunchKernelGGL(kernel_for(lc.feat), dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
+                                   t_whole);
+                hipLaunchKernelGGL(rkern, dim3((unsigned)blocks), dim3(GS_BLOCK), lds, st, a);
                 hipLaunchKernelGGL(gs_round_combine_kernel, dim3(g_comb), dim3(256), 0, st, (const KParams*)dP, r);
             }
         HIPCHK(hipGetLastError());
