@@ -112,6 +112,31 @@ using namespace gsd;
 #ifndef GS_NODE_STEPS
 #define GS_NODE_STEPS 8  // node steps per unrolled node pass (the render kernel, below)
 #endif
+// A wave's issue priority raised (s_setprio level, back to 0 after) while it runs a node pass --
+// a chain of dependent LDS reads and box tests, latency-bound per wave -- and, in kernels whose
+// leaves are not all stationary spheres and whose leaf passes are not C5's mix (staged shading
+// without media or nested BVHs), a leaf pass.  Round 6, MI355X (Msamples/s; none / node
+// 1 / node 1 + leaf 1 / node 2 + leaf 1 / node 3): C4 8 773 / 8 971 / 8 886 / 8 911 / 8 962, C3
+// 13 969 / 13 992 / 14 204 / 14 179 / 14 011, C2 38 267 / 38 279 / 38 385 / 38 365 / 38 450, C1
+// 21 346 / 21 123 / 21 547 / 21 475 / 21 507; none / node 1 / node 1 + leaf 1: C5 7 129 / 7 164 /
+// 7 057, final_scene 2 750 / 2 772 / 2 807, cornell_smoke 9 702 / 9 700 / 9 770, A2 11 074 / - /
+// 11 333 (profiles/r06/ab_wave_priority.txt).  (FEAT: the kernel's template argument where the
+// macros are used.)
+#ifndef GS_PRIO_NODE
+#define GS_PRIO_NODE 1
+#endif
+#ifndef GS_PRIO_LEAF
+#define GS_PRIO_LEAF                                 \
+    ((FEAT & GS_FEAT_SPHLEAF) == 0 &&                \
+             ((FEAT & GS_FEAT_MIXED) == 0 || (FEAT & (GS_FEAT_MEDIA | GS_FEAT_NESTED)) != 0) \
+         ? 1                                         \
+         : 0)
+#endif
+#ifndef GS_PRIO_SHADE
+#define GS_PRIO_SHADE 0
+#endif
+#define GS_PRIO_SET(lvl) do { if (lvl) __builtin_amdgcn_s_setprio(lvl); } while (0)
+#define GS_PRIO_CLR(on) do { if (on) __builtin_amdgcn_s_setprio(0); } while (0)
 __host__ __device__ constexpr int unroll_steps(int feat) { return GS_NODE_STEPS; }
 // The pilot's instantiation: every code path (any scene), plus the counts.
 #define GS_FEAT_PILOT (GS_FEAT_MEDIA | GS_FEAT_NESTED | GS_FEAT_LEAFRUN | GS_FEAT_MIXED | GS_FEAT_VISITS)
@@ -1991,7 +2016,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
             ln_leaf += leaf_pass ? (uint64_t)__popcll(lm) : 0ull;
 #endif
             if (!leaf_pass) {
-                GS_MARK("node_begin");
+                GS_MARK("node_begin"); GS_PRIO_SET(GS_PRIO_NODE);
 // A node pass takes up to GS_NODE_STEPS node steps per lane, unrolled (the loop head's
 // ballots, shade-count and pass-kind tests are paid once per pass, not per node):
 // measured on MI355X C4 (leaf batch 12), Msamples/s: 1 step 5487, 2 5788, 4 6049, 8 6205;
@@ -2106,7 +2131,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #pragma unroll 1
                     for (int nstep = 0; nstep < A.node_steps; nstep++) node_step(slow_t{}, mixed_t{});
                 }
-                GS_MARK("node_end");
+                GS_MARK("node_end"); GS_PRIO_CLR(GS_PRIO_NODE);
             } else if (kNested && __builtin_amdgcn_ballot_w64(cur == THR_RET) != 0) {
                 // Return passes (GS_FEAT_NESTED): a lane whose walk of a BVH under an instance
                 // chain ended (the tree's last links are THR_RET) takes back its top-level ray
@@ -2124,7 +2149,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 }
                 GS_REGION(6, rt0_);  // (stamps: return passes)
             } else if (at_leaf) {
-                GS_MARK("leaf_begin");
+                GS_MARK("leaf_begin"); GS_PRIO_SET(GS_PRIO_LEAF);
                 double scx, scy, scz, sr;
                 uint32_t next, ref;
                 load_tleaf<(FEAT & GS_FEAT_LDSTREE) != 0>(s_leaves, A.tleaves, cur & ~THR_LEAF, A.lds_leaves, scx, scy, scz, sr,
@@ -2357,7 +2382,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                     cur = next;
                 }
                 }  // take_leaf
-                GS_MARK("leaf_end");
+                GS_MARK("leaf_end"); GS_PRIO_CLR(GS_PRIO_LEAF);
             }
             // Nested-BVH kernels and media kernels with sphere leaf runs: the certified test's
             // ray constants are recomputed after a leaf pass (the same function of the same
@@ -2410,7 +2435,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
 #endif
             if constexpr ((FEAT & (GS_FEAT_MIXED | GS_FEAT_MEDIA | GS_FEAT_NESTED)) != 0) {
                 GS_STAMP(r0);
-                GS_MARK("shade_begin");
+                GS_MARK("shade_begin"); GS_PRIO_SET(GS_PRIO_SHADE);
 #if defined(GS_DIAG_DUP) && (GS_DIAG_DUP & 1)
                 {  // cost probe: the shade work twice (the copy's results consumed, its counts double)
                     Ray r2 = ray;
@@ -2433,7 +2458,7 @@ __global__ __launch_bounds__(GS_BLOCK, GS_MIN_WAVES) void gs_render_kernel(KArgs
                 }
                 const ShadeOut s = shade<(FEAT & GS_FEAT_PLAIN) != 0, kSphLeaf, kGeneral>(sc, ray, closest, hit_ref, hinst,
                                                                                         rng, s_cnt, houter);
-                GS_MARK("shade_end");
+                GS_MARK("shade_end"); GS_PRIO_CLR(GS_PRIO_SHADE);
                 GS_REGION(2, r0);
                 if (s.cont) {
                     Tr = Tr * s.col.x;
